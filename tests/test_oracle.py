@@ -1,0 +1,139 @@
+"""Pin the CPU oracle (oracle/tls_oracle.c) before trusting it as the parity
+checker: known-answer tests + every golden vector captured from the reference
+tlslite (tests/golden/records.json).  CPU only."""
+import hashlib
+import hmac
+
+import pytest
+
+from oracle import oracle as O
+from tests.golden_io import case_data, case_keys, rec_pt, wire_matches
+
+
+def test_fips197_aes128_kat():
+    # FIPS-197 Appendix C.1 (verified against the reference rijndael in SURVEY.md §8c)
+    c = O.Conn("aes128", "sha1", (3, 1), bytes.fromhex("000102030405060708090a0b0c0d0e0f"), bytes(16), b"k" * 20)
+    ct = c.encrypt(bytes.fromhex("00112233445566778899aabbccddeeff"))
+    assert ct.hex() == "69c4e0d86a7b0430d8cdb78070b4c55a"
+    d = O.Conn("aes128", "sha1", (3, 1), bytes.fromhex("000102030405060708090a0b0c0d0e0f"), bytes(16), b"k" * 20)
+    assert d.decrypt(ct).hex() == "00112233445566778899aabbccddeeff"
+
+
+def test_fips197_aes256_kat():
+    key = bytes(range(32))
+    c = O.Conn("aes256", "sha1", (3, 1), key, bytes(16), b"k" * 20)
+    assert c.encrypt(bytes.fromhex("00112233445566778899aabbccddeeff")).hex() == "8ea2b7ca516745bfeafc49904b496089"
+
+
+def test_rc4_classic_kat():
+    # "Key"/"Plaintext" -> bbf316e8d940af0ad3; tlslite needs >=16-byte keys (rc4.py:9),
+    # repeating the key 6x leaves the KSA unchanged
+    c = O.Conn("rc4", "sha1", (3, 1), b"Key" * 6, b"", b"k" * 20)
+    assert c.encrypt(b"Plaintext").hex() == "bbf316e8d940af0ad3"
+
+
+def test_des_kats():
+    # FIPS 46 classic single-DES vector via EDE with K1=K2=K3
+    k = bytes.fromhex("133457799BBCDFF1") * 3
+    c = O.Conn("3des", "sha1", (3, 1), k, bytes(8), b"k" * 20)
+    assert c.encrypt(bytes.fromhex("0123456789ABCDEF")).hex() == "85e813540f0ab405"
+    # OpenSSL EVP_des_ede3_cbc cross-check
+    k = bytes.fromhex("0123456789abcdeffedcba987654321089abcdef01234567")
+    c = O.Conn("3des", "sha1", (3, 1), k, bytes(8), b"k" * 20)
+    assert c.encrypt(b"AAAAAAAA").hex() == "75cfa1c273454ec7"
+
+
+@pytest.mark.parametrize("alg", ["sha1", "sha256", "md5"])
+@pytest.mark.parametrize("n", [0, 1, 55, 56, 63, 64, 65, 119, 120, 1000])
+def test_hashes_vs_hashlib(alg, n):
+    data = bytes((i * 7 + 3) & 0xff for i in range(n))
+    assert O.hash_(alg, data) == hashlib.new(alg, data).digest()
+    key = bytes(range(20))
+    assert O.hmac_(alg, key, data) == hmac.new(key, data, alg).digest()
+
+
+def test_hmac_rfc_kats():
+    # RFC 2202 tc1 / RFC 4231 tc1
+    assert O.hmac_("sha1", b"\x0b" * 20, b"Hi There").hex() == "b617318655057264e28bc0b6fb378c8ef146be00"
+    assert O.hmac_("sha256", b"\x0b" * 20, b"Hi There").hex() == \
+        "b0344c61d8db38535ca8afceaf0bf12b881dc200c9833da726e9376c2e32cff7"
+
+
+def _conn_for(case):
+    key, iv, mk, fiv, seq = case_keys(case)
+    return O.Conn.for_suite(case["suite"], tuple(case["version"]), key, iv, mk, fiv, seq)
+
+
+def _check_final(conn, case):
+    f = case["final"]
+    assert conn.seqnum == f["seqnum"]
+    if "cbc_iv" in f:
+        assert conn.iv.hex() == f["cbc_iv"]
+    else:
+        S, i, j = conn.rc4
+        assert (S.hex(), i, j) == (f["rc4_S"], f["rc4_i"], f["rc4_j"])
+
+
+def test_golden_records(golden):
+    n = 0
+    for case in golden:
+        if case["kind"] != "records":
+            continue
+        conn = _conn_for(case)
+        for rec in case["records"]:
+            w = conn.seal(rec_pt(rec), rec["type"], case.get("fault"))
+            assert wire_matches(rec, w), case["name"]
+            n += 1
+        _check_final(conn, case)
+    assert n > 500
+
+
+def oracle_write(conn, data, version, block):
+    """writeAsync (tlsrecordlayer.py:257-295) + BEAST split (:543-550)."""
+    outs = []
+    first = True
+    for s in range(0, len(data), 16384):
+        chunk = data[s:s + 16384]
+        if first and version <= (3, 1) and block:
+            outs.append(conn.seal(chunk[:1]))
+            chunk = chunk[1:]
+        if chunk:
+            outs.append(conn.seal(chunk))
+        first = False
+    return outs
+
+
+def test_golden_write_beast_split(golden):
+    for case in golden:
+        if case["kind"] != "write":
+            continue
+        conn = _conn_for(case)
+        block = O.SUITES[case["suite"]][0] != "rc4"
+        outs = oracle_write(conn, case_data(case), tuple(case["version"]), block)
+        assert len(outs) == len(case["writes"]), case["name"]
+        for w, e in zip(outs, case["writes"]):
+            assert wire_matches(e, w), case["name"]
+        _check_final(conn, case)
+
+
+def test_open_roundtrip_and_tamper(golden):
+    """Oracle open path (tlsrecordlayer.py:958-1044) inverts the golden seals and
+    raises bad_record_mac on the reference's badMAC/badPadding records."""
+    for case in golden:
+        if case["kind"] != "records":
+            continue
+        key, iv, mk, fiv, seq = case_keys(case)
+        rd = O.Conn.for_suite(case["suite"], tuple(case["version"]), key, iv, mk, fiv, seq)
+        for rec in case["records"]:
+            if "wire" not in rec:
+                break  # large record stored as a digest: the read chain cannot continue
+            w = bytes.fromhex(rec["wire"])
+            if not w:
+                continue
+            st, pt = rd.open(w[5:], w[0])
+            effective = case.get("fault") == "badMAC" or (
+                case.get("fault") == "badPadding" and O.SUITES[case["suite"]][0] != "rc4")
+            if effective:
+                assert st == O.ALERT_BAD_RECORD_MAC, case["name"]
+                break
+            assert st == 0 and pt == rec_pt(rec), case["name"]
