@@ -1,0 +1,204 @@
+/*
+ * tlsgpu.h -- C ABI of libtlsgpu.so, the MI355X (gfx950) TLS record-layer
+ * bulk-crypto engine.  Plain pointers and sizes only; no torch/HIP types leak
+ * through (streams and events are opaque handles).
+ *
+ * What each entry point replaces in the reference (trevp/tlslite 0.4.9, paths
+ * relative to the repository root):
+ *
+ *   tlsgpu_conn_state_init ... tlsrecordlayer.py:1127-1149 (_calcPendingStates:
+ *                              createHMAC / createAES / createRC4 /
+ *                              createTripleDES + fixedIVBlock) and
+ *                              mathtls.py:116-151 (createHMAC, MAC_SSL)
+ *   tlsgpu_seal_dev .......... tlsrecordlayer.py:538-617 (_sendMsg seal block:
+ *                              MAC :567-586, explicit IV :594-595, padding
+ *                              :597-606, encrypt :608/:613, header :616-617),
+ *                              batched over many records / connections
+ *   tlsgpu_open_dev .......... tlsrecordlayer.py:958-1044 (_decryptRecord)
+ *   tlsgpu_cipher_dev ........ utils/python_aes.py:20-69, utils/python_rc4.py:25-41,
+ *                              utils/openssl_tripledes.py:29-47 (the stateful
+ *                              cipher-object encrypt/decrypt behind
+ *                              utils/cipherfactory.py:31-102)
+ *   tlsgpu_conn_state_get_* .. the state tlslite keeps in python objects:
+ *                              Python_AES.IV (python_aes.py:44), Python_RC4.S/i/j
+ *                              (python_rc4.py:21-23,36-37), _ConnectionState.seqnum
+ *                              (tlsrecordlayer.py:31-37)
+ *
+ * Conventions: every function returns 0 on success or a negative error code
+ * (TLSGPU_E*).  "_dev" functions take DEVICE pointers and are asynchronous on
+ * the given stream (NULL = the default stream of the current device).
+ */
+#ifndef TLSGPU_H
+#define TLSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TLSGPU_ABI_VERSION 1
+
+/* ---- suite components (tlsrecordlayer.py:1063-1095, constants.py:159-201) */
+enum {
+    TLSGPU_CIPHER_AES128 = 1, /* aes128Suites: key 16, IV 16 */
+    TLSGPU_CIPHER_AES256 = 2, /* aes256Suites: key 32, IV 16 */
+    TLSGPU_CIPHER_RC4 = 3,    /* rc4Suites:    key 16, no IV */
+    TLSGPU_CIPHER_3DES = 4    /* tripleDESSuites: key 24, IV 8 */
+};
+enum {
+    TLSGPU_MAC_SHA1 = 1,   /* shaSuites, 20-byte MAC */
+    TLSGPU_MAC_SHA256 = 2, /* sha256Suites, 32-byte MAC (TLS 1.2 only) */
+    TLSGPU_MAC_MD5 = 3     /* md5Suites, 16-byte MAC */
+};
+/* per-record fault flags (constants.py:310-359; tlsrecordlayer.py:585-586,603-604) */
+enum { TLSGPU_FAULT_BAD_MAC = 1, TLSGPU_FAULT_BAD_PADDING = 2 };
+
+/* error / status codes */
+enum {
+    TLSGPU_OK = 0,
+    TLSGPU_EINVAL = -1,     /* bad argument (key/IV length, size, variant) */
+    TLSGPU_EHIP = -2,       /* HIP runtime error; see tlsgpu_last_error() */
+    TLSGPU_ENODEV = -3,     /* no GPU / bad device ordinal */
+    TLSGPU_ETOOBIG = -4,    /* record body would not fit the 16-bit length (codec.py:19-20) */
+    TLSGPU_EMISMATCH = -5,  /* connection state does not match the launch variant */
+    /* open-path per-record status (alerts, tlsrecordlayer.py:964-1042) */
+    TLSGPU_ALERT_BAD_RECORD_MAC = -20,
+    TLSGPU_ALERT_DECRYPTION_FAILED = -21
+};
+
+/* Launch variant = one (cipher, MAC, SSL3-or-TLS) kernel instantiation.
+ * Records of different variants go in different launches (or streams). */
+#define TLSGPU_VARIANT(cipher, mac, ssl3) ((uint32_t)(cipher) | ((uint32_t)(mac) << 8) | ((uint32_t)((ssl3) ? 1 : 0) << 16))
+
+/* ---- per-connection state: device-resident, updated in place by the
+ * kernels so that consecutive batches equal one long tlslite connection.
+ * Fields are private to the library except through the accessors below. */
+#define TLSGPU_CONN_STATE_BYTES 2048
+typedef struct tlsgpu_conn_state {
+    uint8_t opaque[TLSGPU_CONN_STATE_BYTES];
+} __attribute__((aligned(16))) tlsgpu_conn_state;
+
+/* One record to seal.  Plaintext at pt + pt_off (pt_len bytes); the wire
+ * record (5-byte header + body) is written at wire + wire_off.  Fast path:
+ * pt_off % 16 == 0 and (wire_off + 5) % 16 == 0; any other alignment is
+ * correct but slower.  pt_len == 0 writes nothing and consumes no seqnum
+ * (tlsrecordlayer.py:551-556). */
+typedef struct tlsgpu_record {
+    uint64_t pt_off;
+    uint64_t wire_off;
+    uint32_t pt_len;
+    uint8_t content_type; /* 23 application_data, 21 alert, 22 handshake ... */
+    uint8_t flags;        /* TLSGPU_FAULT_* */
+    uint16_t reserved;
+} tlsgpu_record;
+
+/* A run of records of ONE connection, sealed in order (CBC residue, RC4
+ * keystream and seqnum carried from record to record).  Independent chains
+ * run in parallel; a record must belong to exactly one chain. */
+typedef struct tlsgpu_chain {
+    uint32_t state;    /* index into the states array */
+    uint32_t first;    /* first record index */
+    uint32_t count;    /* number of records */
+    uint32_t reserved;
+} tlsgpu_chain;
+
+/* One record to open.  Body (ciphertext, header already parsed) at
+ * wire + ct_off, ct_len bytes; the plaintext is written at pt + pt_off. */
+typedef struct tlsgpu_open_record {
+    uint64_t ct_off;
+    uint64_t pt_off;
+    uint32_t ct_len;
+    uint8_t content_type;
+    uint8_t reserved[3];
+} tlsgpu_open_record;
+
+/* Raw cipher-object span (factory surface): encrypt/decrypt len bytes of
+ * in + off into out + off with connection state `state`. */
+typedef struct tlsgpu_span {
+    uint64_t off;
+    uint32_t len;
+    uint32_t state;
+} tlsgpu_span;
+
+typedef struct tlsgpu_stream_s *tlsgpu_stream;
+typedef struct tlsgpu_event_s *tlsgpu_event;
+
+/* ---- library / device ---------------------------------------------------- */
+int tlsgpu_abi_version(void);
+const char *tlsgpu_last_error(void);
+int tlsgpu_device_count(int *n);
+int tlsgpu_set_device(int ordinal);
+int tlsgpu_get_device(int *ordinal);
+int tlsgpu_device_synchronize(void);
+/* fills *name (cap bytes) with the device arch name, e.g. "gfx950" */
+int tlsgpu_device_arch(int ordinal, char *name, size_t cap);
+
+/* ---- memory ------------------------------------------------------------- */
+int tlsgpu_malloc(void **dptr, size_t bytes);
+int tlsgpu_free(void *dptr);
+int tlsgpu_host_alloc(void **hptr, size_t bytes); /* pinned host memory */
+int tlsgpu_host_free(void *hptr);
+int tlsgpu_memcpy_h2d(void *dst, const void *src, size_t bytes, tlsgpu_stream s);
+int tlsgpu_memcpy_d2h(void *dst, const void *src, size_t bytes, tlsgpu_stream s);
+int tlsgpu_memcpy_d2d(void *dst, const void *src, size_t bytes, tlsgpu_stream s);
+int tlsgpu_memset(void *dptr, int value, size_t bytes, tlsgpu_stream s);
+
+/* ---- streams / events ---------------------------------------------------- */
+int tlsgpu_stream_create(tlsgpu_stream *s);
+int tlsgpu_stream_destroy(tlsgpu_stream s);
+int tlsgpu_stream_synchronize(tlsgpu_stream s);
+int tlsgpu_event_create(tlsgpu_event *e);
+int tlsgpu_event_destroy(tlsgpu_event e);
+int tlsgpu_event_record(tlsgpu_event e, tlsgpu_stream s);
+int tlsgpu_event_synchronize(tlsgpu_event e);
+int tlsgpu_event_elapsed_ms(float *ms, tlsgpu_event start, tlsgpu_event stop);
+
+/* ---- connection state (host-side construction, no GPU needed) ------------
+ * Equivalent of _calcPendingStates' per-direction state: key schedule of the
+ * bulk cipher, HMAC ipad/opad midstates (or SSL3 MAC_SSL prefix state), CBC
+ * IV, TLS>=1.1 fixedIVBlock, RC4 KSA, seqnum.  Validation mirrors the
+ * reference: AES key 16/32 + IV 16 (aes.py:7-13), 3DES key 24 + IV 8
+ * (tripledes.py:8-13), RC4 key 16..256 + empty IV (rc4.py:9-10,
+ * cipherfactory.py:70-71); SHA256 only at TLS 1.2 (constants.py:204-210). */
+int tlsgpu_conn_state_init(tlsgpu_conn_state *st, int cipher, int mac, int ver_major, int ver_minor,
+                           const uint8_t *key, size_t key_len, const uint8_t *iv, size_t iv_len,
+                           const uint8_t *mac_key, size_t mac_key_len, const uint8_t *fixed_iv,
+                           size_t fixed_iv_len, uint64_t seqnum);
+/* raw cipher context (cipher-object surface: no MAC, version 0.0) */
+int tlsgpu_cipher_state_init(tlsgpu_conn_state *st, int cipher, const uint8_t *key, size_t key_len,
+                             const uint8_t *iv, size_t iv_len);
+int tlsgpu_conn_state_set_seqnum(tlsgpu_conn_state *st, uint64_t seqnum);
+int tlsgpu_conn_state_set_iv(tlsgpu_conn_state *st, const uint8_t *iv, size_t iv_len);
+int tlsgpu_conn_state_get_seqnum(const tlsgpu_conn_state *st, uint64_t *seqnum);
+int tlsgpu_conn_state_get_iv(const tlsgpu_conn_state *st, uint8_t *iv, size_t cap, size_t *iv_len);
+int tlsgpu_conn_state_get_rc4(const tlsgpu_conn_state *st, uint8_t S[256], uint32_t *i, uint32_t *j);
+int tlsgpu_conn_state_variant(const tlsgpu_conn_state *st, uint32_t *variant);
+/* wire length of a sealed record of pt_len bytes for this state (0 if pt_len==0) */
+int tlsgpu_seal_wire_len(const tlsgpu_conn_state *st, uint32_t pt_len, uint32_t *wire_len);
+
+/* ---- batch seal / open (device pointers, async on stream) ---------------
+ * wire_len[r] receives the bytes written for record r (header included), 0
+ * for an empty record, or a negative TLSGPU_E* code.  All chains of one
+ * launch must use connection states of `variant`. */
+int tlsgpu_seal_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_record *records,
+                    const uint8_t *pt, uint8_t *wire, tlsgpu_conn_state *states, int32_t *wire_len,
+                    uint32_t variant, tlsgpu_stream s);
+/* status[r] = plaintext length, or TLSGPU_ALERT_* */
+int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_open_record *records,
+                    const uint8_t *wire, uint8_t *pt, tlsgpu_conn_state *states, int32_t *status,
+                    uint32_t variant, tlsgpu_stream s);
+/* raw stateful encrypt (decrypt=0) / decrypt (decrypt=1) of spans; one span
+ * per state per launch (a state's spans in one launch run in array order). */
+int tlsgpu_cipher_dev(const tlsgpu_span *spans, uint32_t nspans, const uint8_t *in, uint8_t *out,
+                      tlsgpu_conn_state *states, int cipher, int decrypt, tlsgpu_stream s);
+
+/* ---- synthetic input (bench / tests): byte i = byte (i&7) of
+ * splitmix64(seed + (i>>3)), little-endian, for i in [start, start+bytes). */
+int tlsgpu_fill_pattern(uint8_t *dptr, size_t bytes, uint64_t seed, uint64_t start, tlsgpu_stream s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TLSGPU_H */

@@ -107,7 +107,8 @@ class Conn:
         L = lib()
         cap = len(pt) + 128
         out = ctypes.create_string_buffer(cap)
-        n = L.ora_seal(self.buf, ctype, bytes(pt), len(pt), FAULT[fault], out, cap)
+        fl = fault if isinstance(fault, int) else FAULT[fault]
+        n = L.ora_seal(self.buf, ctype, bytes(pt), len(pt), fl, out, cap)
         if n < 0:
             raise ValueError("seal error %d" % n)
         return out.raw[:n]

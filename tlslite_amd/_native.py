@@ -1,0 +1,123 @@
+"""ctypes binding of libtlsgpu.so (include/tlsgpu.h).
+
+There is no CPU fallback: if the HIP library is missing this module raises
+ImportError, and every compute call goes to the gfx950 kernels.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libtlsgpu.so")
+
+# constants mirrored from include/tlsgpu.h
+CIPHER_AES128, CIPHER_AES256, CIPHER_RC4, CIPHER_3DES = 1, 2, 3, 4
+MAC_SHA1, MAC_SHA256, MAC_MD5 = 1, 2, 3
+FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
+OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH = 0, -1, -2, -3, -4, -5
+ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED = -20, -21
+CONN_STATE_BYTES = 2048
+
+
+def variant(cipher, mac, ssl3):
+    return cipher | (mac << 8) | ((1 if ssl3 else 0) << 16)
+
+
+class Record(ctypes.Structure):  # tlsgpu_record
+    _fields_ = [("pt_off", ctypes.c_uint64), ("wire_off", ctypes.c_uint64), ("pt_len", ctypes.c_uint32),
+                ("content_type", ctypes.c_uint8), ("flags", ctypes.c_uint8), ("reserved", ctypes.c_uint16)]
+
+
+class Chain(ctypes.Structure):  # tlsgpu_chain
+    _fields_ = [("state", ctypes.c_uint32), ("first", ctypes.c_uint32), ("count", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class OpenRecord(ctypes.Structure):  # tlsgpu_open_record
+    _fields_ = [("ct_off", ctypes.c_uint64), ("pt_off", ctypes.c_uint64), ("ct_len", ctypes.c_uint32),
+                ("content_type", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 3)]
+
+
+class Span(ctypes.Structure):  # tlsgpu_span
+    _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint32), ("state", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(Record) == 24 and ctypes.sizeof(Chain) == 16
+assert ctypes.sizeof(OpenRecord) == 24 and ctypes.sizeof(Span) == 16
+
+# (name, restype, argtypes) for every symbol of include/tlsgpu.h
+_vp, _u8p, _sz, _i, _u32, _u64 = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
+SIGNATURES = [
+    ("tlsgpu_abi_version", _i, []),
+    ("tlsgpu_last_error", ctypes.c_char_p, []),
+    ("tlsgpu_device_count", _i, [ctypes.POINTER(_i)]),
+    ("tlsgpu_set_device", _i, [_i]),
+    ("tlsgpu_get_device", _i, [ctypes.POINTER(_i)]),
+    ("tlsgpu_device_synchronize", _i, []),
+    ("tlsgpu_device_arch", _i, [_i, ctypes.c_char_p, _sz]),
+    ("tlsgpu_malloc", _i, [ctypes.POINTER(_vp), _sz]),
+    ("tlsgpu_free", _i, [_vp]),
+    ("tlsgpu_host_alloc", _i, [ctypes.POINTER(_vp), _sz]),
+    ("tlsgpu_host_free", _i, [_vp]),
+    ("tlsgpu_memcpy_h2d", _i, [_vp, _vp, _sz, _vp]),
+    ("tlsgpu_memcpy_d2h", _i, [_vp, _vp, _sz, _vp]),
+    ("tlsgpu_memcpy_d2d", _i, [_vp, _vp, _sz, _vp]),
+    ("tlsgpu_memset", _i, [_vp, _i, _sz, _vp]),
+    ("tlsgpu_stream_create", _i, [ctypes.POINTER(_vp)]),
+    ("tlsgpu_stream_destroy", _i, [_vp]),
+    ("tlsgpu_stream_synchronize", _i, [_vp]),
+    ("tlsgpu_event_create", _i, [ctypes.POINTER(_vp)]),
+    ("tlsgpu_event_destroy", _i, [_vp]),
+    ("tlsgpu_event_record", _i, [_vp, _vp]),
+    ("tlsgpu_event_synchronize", _i, [_vp]),
+    ("tlsgpu_event_elapsed_ms", _i, [ctypes.POINTER(ctypes.c_float), _vp, _vp]),
+    ("tlsgpu_conn_state_init", _i, [_vp, _i, _i, _i, _i, _u8p, _sz, _u8p, _sz, _u8p, _sz, _u8p, _sz, _u64]),
+    ("tlsgpu_cipher_state_init", _i, [_vp, _i, _u8p, _sz, _u8p, _sz]),
+    ("tlsgpu_conn_state_set_seqnum", _i, [_vp, _u64]),
+    ("tlsgpu_conn_state_set_iv", _i, [_vp, _u8p, _sz]),
+    ("tlsgpu_conn_state_get_seqnum", _i, [_vp, ctypes.POINTER(_u64)]),
+    ("tlsgpu_conn_state_get_iv", _i, [_vp, _u8p, _sz, ctypes.POINTER(_sz)]),
+    ("tlsgpu_conn_state_get_rc4", _i, [_vp, _u8p, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
+    ("tlsgpu_conn_state_variant", _i, [_vp, ctypes.POINTER(_u32)]),
+    ("tlsgpu_seal_wire_len", _i, [_vp, _u32, ctypes.POINTER(_u32)]),
+    ("tlsgpu_seal_dev", _i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("tlsgpu_cipher_dev", _i, [_vp, _u32, _vp, _vp, _vp, _i, _i, _vp]),
+    ("tlsgpu_fill_pattern", _i, [_vp, _sz, _u64, _u64, _vp]),
+]
+
+
+class TLSGPUError(RuntimeError):
+    def __init__(self, code, where):
+        msg = last_error()
+        super().__init__("%s failed (%d): %s" % (where, code, msg))
+        self.code = code
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libtlsgpu.so is not built (%s); run `python -c \"import __graft_entry__ as g; g.build()\"`"
+                          % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def last_error():
+    s = lib.tlsgpu_last_error()
+    return s.decode(errors="replace") if s else ""
+
+
+def check(rc, where):
+    if rc != 0:
+        raise TLSGPUError(rc, where)
+    return rc
+
+
+def call(name, *args):
+    return check(getattr(lib, name)(*args), name)

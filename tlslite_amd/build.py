@@ -1,0 +1,62 @@
+"""Build libtlsgpu.so in-tree (tlslite_amd/lib/) with hipcc for gfx950.
+
+The shared library is the product: the C ABI of include/tlsgpu.h, the gfx950
+kernels, and the host-side state construction.  It is git-ignored but travels
+to the GPU box with the repository snapshot.
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libtlsgpu.so")
+ARCH = os.environ.get("TLSGPU_ARCH", "gfx950")
+
+SOURCES = ["tg_kernels.hip", "tg_api.hip"]
+HEADERS = ["tg_common.h", "tg_hash.h", "tg_device.h", "tg_launch.h"]
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False, extra_flags=()):
+    os.makedirs(LIBDIR, exist_ok=True)
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", "tlsgpu.h")]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objs = []
+    hipcc = _hipcc()
+    flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
+             "-munsafe-fp-atomics"] + list(extra_flags)
+    for s in srcs:
+        o = os.path.join(LIBDIR, os.path.basename(s) + ".o")
+        cmd = [hipcc] + flags + ["-c", s, "-o", o]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+        objs.append(o)
+    tmp = LIB + ".tmp"
+    cmd = [hipcc, "-shared", "--offload-arch=" + ARCH, "-o", tmp] + objs
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose=True)
+    print(LIB)

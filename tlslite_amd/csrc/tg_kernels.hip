@@ -1,0 +1,370 @@
+// tg_kernels.hip -- gfx950 kernels of libtlsgpu.so:
+//   seal_kernel    fused per-record  MAC -> pad -> CBC/RC4 encrypt -> header,
+//                  one lane per connection chain (tlsrecordlayer.py:538-617)
+//   cipher_kernel  raw stateful CBC / RC4 encrypt+decrypt for the
+//                  cipher-object surface (python_aes.py:20-69, python_rc4.py:25-41)
+//   fill_kernel    deterministic synthetic input (splitmix64 byte stream)
+#include "tg_device.h"
+#include "tg_launch.h"
+
+namespace tg {
+
+template <class C>
+struct CipherTraits;
+template <>
+struct CipherTraits<AesCbc<10>> {
+    static constexpr int ID = TLSGPU_CIPHER_AES128;
+    static constexpr uint32_t LDS = AES_LDS_BYTES;
+};
+template <>
+struct CipherTraits<AesCbc<14>> {
+    static constexpr int ID = TLSGPU_CIPHER_AES256;
+    static constexpr uint32_t LDS = AES_LDS_BYTES;
+};
+template <>
+struct CipherTraits<TdesCbc> {
+    static constexpr int ID = TLSGPU_CIPHER_3DES;
+    static constexpr uint32_t LDS = DES_LDS_BYTES;
+};
+template <>
+struct CipherTraits<Rc4Stream> {
+    static constexpr int ID = TLSGPU_CIPHER_RC4;
+    static constexpr uint32_t LDS = RC4_LDS_BYTES_PER_WAVE * (SEAL_BLOCK / 64);
+};
+
+template <class C>
+__device__ __forceinline__ void fill_tables(uint32_t* lds) {
+    if constexpr (CipherTraits<C>::ID == TLSGPU_CIPHER_AES128 || CipherTraits<C>::ID == TLSGPU_CIPHER_AES256)
+        aes_lds_fill(lds, false);
+    else if constexpr (CipherTraits<C>::ID == TLSGPU_CIPHER_3DES)
+        des_lds_fill(lds);
+}
+
+// One lane = one chain (a connection's ordered run of records).
+template <class C, int MAC, bool SSL3>
+__global__ void __launch_bounds__(SEAL_BLOCK) seal_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
+                                                         const tlsgpu_record* __restrict__ recs,
+                                                         const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
+                                                         ConnState* __restrict__ states,
+                                                         int32_t* __restrict__ wire_len) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    fill_tables<C>(lds);
+    __syncthreads();
+
+    const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cid >= nchains) return;
+    const tlsgpu_chain ch = chains[cid];
+    ConnState* st = states + ch.state;
+    using M = RecMac<MAC, SSL3>;
+    constexpr int DL = M::DL;
+    constexpr int BS = C::BS;
+
+    if (st->cipher != (uint32_t)CipherTraits<C>::ID || st->mac != (uint32_t)MAC || st->ssl3 != (SSL3 ? 1u : 0u) ||
+        st->raw) {
+        for (uint32_t k = 0; k < ch.count; k++) wire_len[ch.first + k] = TLSGPU_EMISMATCH;
+        return;
+    }
+    C cipher;
+    cipher.load(st, lds);
+    uint64_t seq = st->seqnum;
+    const uint32_t E = (!C::STREAM && st->explicit_iv) ? (uint32_t)BS : 0u;
+    const uint32_t vmaj = st->vmaj, vmin = st->vmin;
+
+    for (uint32_t k = 0; k < ch.count; k++) {
+        const tlsgpu_record R = recs[ch.first + k];
+        const uint32_t n = R.pt_len;
+        if (n == 0) {  // empty record: nothing sent, no seqnum consumed (tlsrecordlayer.py:551-556)
+            wire_len[ch.first + k] = 0;
+            continue;
+        }
+        uint32_t body;
+        if (C::STREAM) {
+            body = n + DL;
+        } else {
+            uint32_t cur = E + n + DL;
+            body = cur + (BS - (cur % BS));  // pad = BS-1-(cur%BS), plus the length byte
+        }
+        if (body > 0xffffu) {
+            wire_len[ch.first + k] = TLSGPU_ETOOBIG;
+            continue;
+        }
+        const uint8_t* P = pt + R.pt_off;
+        uint8_t* W = wire + R.wire_off;
+        uint8_t* B = W + 5;
+
+        M mac;
+        mac.begin(st, seq, R.content_type, n);
+        if (!C::STREAM && E) {  // TLS>=1.1: fixedIVBlock encrypted with the chained residue
+            uint32_t blk[4] = {st->fixed_iv[0], st->fixed_iv[1], st->fixed_iv[2], st->fixed_iv[3]};
+            if constexpr (!C::STREAM) {
+                cipher.enc_block(blk);
+                cipher.store_block(B, blk);
+            }
+        }
+        const uint32_t nfull = n >> 6;
+        uint8_t* Bp = B + E;
+        for (uint32_t c = 0; c < nfull; c++) {
+            uint32_t cur[16];
+            load64(P + 64 * c, cur);
+            mac.update(cur);
+            cipher.enc64(cur);
+            store64(Bp + 64 * c, cur);
+        }
+        const uint32_t r = n & 63;
+        uint32_t tail[16];
+        load_partial(P + 64 * nfull, r, tail);
+        uint32_t m[8];
+        mac.finish(tail, (int)r, n, st, m);
+        if (R.flags & TLSGPU_FAULT_BAD_MAC) m[0] = (m[0] & ~0xffu) | ((m[0] + 1u) & 0xffu);
+
+        // tail stream = P[64*nfull ..) | MAC | pad, staged in a private buffer
+        uint32_t tb[32];
+#pragma unroll
+        for (int q = 0; q < 16; q++) tb[q] = tail[q];
+#pragma unroll
+        for (int q = 16; q < 32; q++) tb[q] = 0;
+        uint8_t* tbb = reinterpret_cast<uint8_t*>(tb);
+#pragma unroll
+        for (int i = 0; i < DL; i++) tbb[r + i] = (uint8_t)(m[i >> 2] >> (8 * (i & 3)));
+        uint8_t* Bt = Bp + 64 * nfull;
+        if constexpr (!C::STREAM) {
+            const uint32_t padl = BS - 1 - ((r + DL) % BS);
+            for (uint32_t i = 0; i <= padl; i++) tbb[r + DL + i] = (uint8_t)padl;
+            if (R.flags & TLSGPU_FAULT_BAD_PADDING) tbb[r + DL] = (uint8_t)(padl + 1);
+            const uint32_t T = r + DL + padl + 1;
+            for (uint32_t off = 0; off < T; off += BS) {
+                uint32_t blk[4];
+#pragma unroll
+                for (int q = 0; q < BS / 4; q++) blk[q] = tb[(off >> 2) + q];
+                cipher.enc_block(blk);
+                cipher.store_block(Bt + off, blk);
+            }
+        } else {
+            const uint32_t T = r + DL;
+            for (uint32_t p = 0; p < T; p++) Bt[p] = (uint8_t)(tbb[p] ^ cipher.R.ks());
+        }
+        W[0] = R.content_type;
+        W[1] = (uint8_t)vmaj;
+        W[2] = (uint8_t)vmin;
+        W[3] = (uint8_t)(body >> 8);
+        W[4] = (uint8_t)body;
+        wire_len[ch.first + k] = (int32_t)(body + 5);
+        seq++;
+    }
+    st->seqnum = seq;
+    cipher.save(st);
+}
+
+// ---------------------------------------------------------------- raw cipher object
+template <int NR>
+struct AesCbcDec {
+    uint32_t dk[4 * (NR + 1)];
+    uint32_t iv[4];
+    AesLds L;
+    __device__ __forceinline__ void load(const ConnState* st, const void* lds) {
+        L.init(lds);
+#pragma unroll
+        for (int k = 0; k < 4 * (NR + 1); k++) dk[k] = st->dk[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) iv[k] = st->iv[k];
+    }
+    __device__ __forceinline__ void save(ConnState* st) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) st->iv[k] = iv[k];
+    }
+    __device__ __forceinline__ void dec_block(uint32_t* d) {
+        uint32_t c[4] = {d[0], d[1], d[2], d[3]};
+        uint32_t s[4] = {d[0], d[1], d[2], d[3]};
+        aes_decrypt<NR>(s, dk, L);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            d[k] = s[k] ^ iv[k];
+            iv[k] = c[k];
+        }
+    }
+};
+
+template <int CIPHER, bool DEC>
+__global__ void __launch_bounds__(SEAL_BLOCK) cipher_kernel(const tlsgpu_span* __restrict__ spans, uint32_t nspans,
+                                                           const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                           ConnState* __restrict__ states) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr bool AES = CIPHER == TLSGPU_CIPHER_AES128 || CIPHER == TLSGPU_CIPHER_AES256;
+    constexpr int NR = CIPHER == TLSGPU_CIPHER_AES256 ? 14 : 10;
+    if constexpr (AES) aes_lds_fill(lds, DEC);
+    else if constexpr (CIPHER == TLSGPU_CIPHER_3DES) des_lds_fill(lds);
+    __syncthreads();
+    const uint32_t sid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sid >= nspans) return;
+    const tlsgpu_span sp = spans[sid];
+    ConnState* st = states + sp.state;
+    if (st->cipher != (uint32_t)CIPHER) return;
+    const uint8_t* src = in + sp.off;
+    uint8_t* dst = out + sp.off;
+    if constexpr (AES && !DEC) {
+        AesCbc<NR> c;
+        c.load(st, lds);
+        for (uint32_t off = 0; off + 16 <= sp.len; off += 16) {
+            uint32_t d[4];
+            load16(src + off, d);
+            c.enc_block(d);
+            store16(dst + off, d);
+        }
+        c.save(st);
+    } else if constexpr (AES && DEC) {
+        AesCbcDec<NR> c;
+        c.load(st, lds);
+        for (uint32_t off = 0; off + 16 <= sp.len; off += 16) {
+            uint32_t d[4];
+            load16(src + off, d);
+            c.dec_block(d);
+            store16(dst + off, d);
+        }
+        c.save(st);
+    } else if constexpr (CIPHER == TLSGPU_CIPHER_3DES) {
+        TdesCbc c;
+        c.load(st, lds);
+        for (uint32_t off = 0; off + 8 <= sp.len; off += 8) {
+            uint32_t d[2];
+            load8(src + off, d);
+            if (!DEC) {
+                c.enc_block(d);
+            } else {
+                uint32_t c0 = d[0], c1 = d[1];
+                uint32_t hi = bswap32(d[0]), lo = bswap32(d[1]);
+                tdes_block<true>(hi, lo, c.ks, c.L);
+                d[0] = bswap32(hi) ^ c.iv[0];
+                d[1] = bswap32(lo) ^ c.iv[1];
+                c.iv[0] = c0;
+                c.iv[1] = c1;
+            }
+            store8(dst + off, d);
+        }
+        c.save(st);
+    } else {
+        Rc4Stream c;
+        c.load(st, lds);
+        for (uint32_t off = 0; off < sp.len; off++) dst[off] = (uint8_t)(src[off] ^ c.R.ks());
+        c.save(st);
+    }
+}
+
+// ---------------------------------------------------------------- synthetic input
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void fill_kernel(uint8_t* __restrict__ p, size_t bytes, uint64_t seed, uint64_t start) {
+    size_t i0 = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 16;
+    if (i0 >= bytes) return;
+    uint32_t d[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 16; b++) {
+        uint64_t g = start + i0 + b;
+        uint32_t v = (uint32_t)(splitmix64(seed + (g >> 3)) >> (8 * (g & 7))) & 0xffu;
+        d[b >> 2] |= v << (8 * (b & 3));
+    }
+    if (i0 + 16 <= bytes) {
+        store16(p + i0, d);
+    } else {
+        for (size_t b = 0; i0 + b < bytes; b++) p[i0 + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
+// ---------------------------------------------------------------- launchers
+template <class K>
+static hipError_t set_lds(K kern, uint32_t bytes) {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)bytes);
+}
+
+template <class C, int MAC, bool SSL3>
+static hipError_t launch_seal_t(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                                const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
+                                hipStream_t s) {
+    auto kern = seal_kernel<C, MAC, SSL3>;
+    constexpr uint32_t lds = CipherTraits<C>::LDS;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = set_lds(kern, lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    dim3 grid((nchains + SEAL_BLOCK - 1) / SEAL_BLOCK);
+    hipLaunchKernelGGL(kern, grid, dim3(SEAL_BLOCK), lds, s, chains, nchains, recs, pt, wire, states, wire_len);
+    return hipGetLastError();
+}
+
+hipError_t launch_seal(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                       const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len, hipStream_t s,
+                       bool* known) {
+    *known = true;
+#define TG_SEAL_CASE(CIPHER_ID, CTYPE, MAC_ID, SSL3)                                                      \
+    if (variant == TLSGPU_VARIANT(CIPHER_ID, MAC_ID, SSL3))                                               \
+        return launch_seal_t<CTYPE, MAC_ID, SSL3>(chains, nchains, recs, pt, wire, states, wire_len, s);
+    // TLS 1.0-1.2 HMAC suites (constants.py:159-201)
+    TG_SEAL_CASE(TLSGPU_CIPHER_AES128, AesCbc<10>, TLSGPU_MAC_SHA1, false)
+    TG_SEAL_CASE(TLSGPU_CIPHER_AES256, AesCbc<14>, TLSGPU_MAC_SHA1, false)
+    TG_SEAL_CASE(TLSGPU_CIPHER_AES128, AesCbc<10>, TLSGPU_MAC_SHA256, false)
+    TG_SEAL_CASE(TLSGPU_CIPHER_AES256, AesCbc<14>, TLSGPU_MAC_SHA256, false)
+    TG_SEAL_CASE(TLSGPU_CIPHER_3DES, TdesCbc, TLSGPU_MAC_SHA1, false)
+    TG_SEAL_CASE(TLSGPU_CIPHER_RC4, Rc4Stream, TLSGPU_MAC_SHA1, false)
+    TG_SEAL_CASE(TLSGPU_CIPHER_RC4, Rc4Stream, TLSGPU_MAC_MD5, false)
+    // SSL 3.0 MAC_SSL suites (mathtls.py:125-151)
+    TG_SEAL_CASE(TLSGPU_CIPHER_AES128, AesCbc<10>, TLSGPU_MAC_SHA1, true)
+    TG_SEAL_CASE(TLSGPU_CIPHER_AES256, AesCbc<14>, TLSGPU_MAC_SHA1, true)
+    TG_SEAL_CASE(TLSGPU_CIPHER_3DES, TdesCbc, TLSGPU_MAC_SHA1, true)
+    TG_SEAL_CASE(TLSGPU_CIPHER_RC4, Rc4Stream, TLSGPU_MAC_SHA1, true)
+    TG_SEAL_CASE(TLSGPU_CIPHER_RC4, Rc4Stream, TLSGPU_MAC_MD5, true)
+#undef TG_SEAL_CASE
+    *known = false;
+    return hipSuccess;
+}
+
+template <int CIPHER, bool DEC>
+static hipError_t launch_cipher_t(const tlsgpu_span* spans, uint32_t n, const uint8_t* in, uint8_t* out,
+                                  ConnState* states, hipStream_t s) {
+    auto kern = cipher_kernel<CIPHER, DEC>;
+    constexpr bool AES = CIPHER == TLSGPU_CIPHER_AES128 || CIPHER == TLSGPU_CIPHER_AES256;
+    constexpr uint32_t lds = AES ? (DEC ? AES_DEC_LDS_BYTES : AES_LDS_BYTES)
+                                 : CIPHER == TLSGPU_CIPHER_3DES ? DES_LDS_BYTES
+                                                                : RC4_LDS_BYTES_PER_WAVE * (SEAL_BLOCK / 64);
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = set_lds(kern, lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    dim3 grid((n + SEAL_BLOCK - 1) / SEAL_BLOCK);
+    hipLaunchKernelGGL(kern, grid, dim3(SEAL_BLOCK), lds, s, spans, n, in, out, states);
+    return hipGetLastError();
+}
+
+hipError_t launch_cipher(int cipher, int dec, const tlsgpu_span* spans, uint32_t n, const uint8_t* in, uint8_t* out,
+                         ConnState* states, hipStream_t s, bool* known) {
+    *known = true;
+#define TG_CIPHER_CASE(ID)                                                                     \
+    if (cipher == ID)                                                                          \
+        return dec ? launch_cipher_t<ID, true>(spans, n, in, out, states, s)                   \
+                   : launch_cipher_t<ID, false>(spans, n, in, out, states, s);
+    TG_CIPHER_CASE(TLSGPU_CIPHER_AES128)
+    TG_CIPHER_CASE(TLSGPU_CIPHER_AES256)
+    TG_CIPHER_CASE(TLSGPU_CIPHER_3DES)
+    TG_CIPHER_CASE(TLSGPU_CIPHER_RC4)
+#undef TG_CIPHER_CASE
+    *known = false;
+    return hipSuccess;
+}
+
+hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, hipStream_t s) {
+    size_t threads = (bytes + 15) / 16;
+    dim3 grid((unsigned)((threads + 255) / 256));
+    if (threads == 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_kernel, grid, dim3(256), 0, s, p, bytes, seed, start);
+    return hipGetLastError();
+}
+
+}  // namespace tg

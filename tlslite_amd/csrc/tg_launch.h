@@ -1,0 +1,17 @@
+// tg_launch.h -- kernel launchers exported from tg_kernels.hip to the C ABI
+// layer (tg_api.hip).
+#pragma once
+#include "tg_common.h"
+
+namespace tg {
+
+constexpr int SEAL_BLOCK = 256;  // one lane per chain, 4 waves per workgroup
+
+hipError_t launch_seal(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                       const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len, hipStream_t s,
+                       bool* known);
+hipError_t launch_cipher(int cipher, int dec, const tlsgpu_span* spans, uint32_t n, const uint8_t* in, uint8_t* out,
+                         ConnState* states, hipStream_t s, bool* known);
+hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, hipStream_t s);
+
+}  // namespace tg

@@ -1,0 +1,182 @@
+"""Batched TLS record seal on the GPU -- the drop-in for the seal block of
+tlslite's `TLSRecordLayer._sendMsg` (tlslite/tlsrecordlayer.py:538-617) and
+the fragmentation of `writeAsync` (:257-295).
+
+Two levels:
+  * `seal(states, records)`      host buffers in, wire bytes out (copies to HBM,
+                                 one kernel launch per suite variant, copies back)
+  * `seal_dev(...)`              device-resident arenas, no copies: the
+                                 throughput path used by bench.py
+"""
+import ctypes
+from collections import OrderedDict
+
+import numpy as np
+
+from . import _native as N
+from .constants import ContentType
+from .device import DeviceBuffer, synchronize
+from .state import STATE_BYTES, pack_states, unpack_states
+
+PT_ALIGN = 16
+WIRE_BODY_ALIGN = 16  # record bodies start 16-byte aligned: wire_off % 16 == 11
+MAX_FRAGMENT = 16384  # tlsrecordlayer.py:273
+
+
+def plan_write(data, version, block_cipher, max_fragment=MAX_FRAGMENT):
+    """Split one write() into record payloads exactly as writeAsync does
+    (tlsrecordlayer.py:257-295), including the TLS<=1.0 block-cipher 1/n-1
+    split of the first fragment (:543-550).  Empty payloads are dropped: the
+    reference emits nothing for them (:551-556)."""
+    out = []
+    first = True
+    for s in range(0, len(data), max_fragment):
+        chunk = bytes(data[s:s + max_fragment])
+        if first and tuple(version) <= (3, 1) and block_cipher:
+            out.append(chunk[:1])
+            chunk = chunk[1:]
+        if chunk:
+            out.append(chunk)
+        first = False
+    return out
+
+
+def wire_offsets(wire_lens):
+    """Slot layout for a wire arena: each record's 5-byte header at
+    off % 16 == 11 so that its body is 16-byte aligned."""
+    offs = np.zeros(len(wire_lens), dtype=np.uint64)
+    pos = 11
+    for i, n in enumerate(wire_lens):
+        offs[i] = pos
+        pos += int(n)
+        pos += (11 - pos) % WIRE_BODY_ALIGN
+    return offs, pos
+
+
+def make_records(pt_off, wire_off, pt_len, content_type=ContentType.application_data, flags=0):
+    n = len(pt_len)
+    recs = (N.Record * n)()
+    a = np.frombuffer(recs, dtype=np.uint8).reshape(n, 24)
+    a[:, 0:8] = np.asarray(pt_off, dtype=np.uint64).reshape(n, 1).view(np.uint8)
+    a[:, 8:16] = np.asarray(wire_off, dtype=np.uint64).reshape(n, 1).view(np.uint8)
+    a[:, 16:20] = np.asarray(pt_len, dtype=np.uint32).reshape(n, 1).view(np.uint8)
+    a[:, 20] = np.broadcast_to(np.asarray(content_type, dtype=np.uint8), (n,))
+    a[:, 21] = np.broadcast_to(np.asarray(flags, dtype=np.uint8), (n,))
+    a[:, 22:24] = 0
+    return recs
+
+
+def make_chains(state_idx, first, count):
+    n = len(state_idx)
+    ch = (N.Chain * n)()
+    a = np.frombuffer(ch, dtype=np.uint32).reshape(n, 4)
+    a[:, 0] = state_idx
+    a[:, 1] = first
+    a[:, 2] = count
+    a[:, 3] = 0
+    return ch
+
+
+def seal_dev(chains, nchains, records, pt, wire, states, wire_len, variant, stream=None):
+    """Device-resident batch seal (all pointers are DeviceBuffer / addresses)."""
+    def p(x):
+        return x.ptr if isinstance(x, DeviceBuffer) else ctypes.c_void_p(x)
+    N.call("tlsgpu_seal_dev", p(chains), nchains, p(records), p(pt), p(wire), p(states), p(wire_len), variant,
+           stream.handle if stream is not None else None)
+
+
+def seal(states, records, stream=None):
+    """Seal records on the GPU.
+
+    states:  list of ConnectionState (updated in place: seqnum, CBC residue, RC4)
+    records: list of (state_index, payload, content_type=23, flags=0); records
+             of one state are sealed in list order, like successive _sendMsg calls.
+    Returns the list of wire records (b"" for an empty payload).
+    """
+    norm = []
+    for r in records:
+        si, payload = r[0], bytes(r[1])
+        ct = r[2] if len(r) > 2 else ContentType.application_data
+        fl = r[3] if len(r) > 3 else 0
+        norm.append((si, payload, ct, fl))
+    nrec = len(norm)
+    if nrec == 0:
+        return []
+    by_state = OrderedDict()
+    for i, (si, _, _, _) in enumerate(norm):
+        by_state.setdefault(si, []).append(i)
+    # descriptor order: chains contiguous
+    order = [i for idxs in by_state.values() for i in idxs]
+    pos_of = {i: k for k, i in enumerate(order)}
+    wlen = []
+    for i in order:
+        si, payload, _, _ = norm[i]
+        n = len(payload)
+        try:
+            wlen.append(states[si].wire_len(n))
+        except N.TLSGPUError as e:
+            if e.code == N.ETOOBIG:
+                raise ValueError("Can't represent value in specified length")  # codec.py:19-20
+            raise
+    pt_off = np.zeros(nrec, dtype=np.uint64)
+    pos = 0
+    for k, i in enumerate(order):
+        pt_off[k] = pos
+        pos += len(norm[i][1])
+        pos += (-pos) % PT_ALIGN
+    pt_total = max(pos, 16)
+    wire_off, wire_total = wire_offsets(wlen)
+    pt_host = np.zeros(pt_total, dtype=np.uint8)
+    for k, i in enumerate(order):
+        b = norm[i][1]
+        if b:
+            pt_host[int(pt_off[k]):int(pt_off[k]) + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    recs = make_records(pt_off, wire_off, [len(norm[i][1]) for i in order], [norm[i][2] for i in order],
+                        [norm[i][3] for i in order])
+    # chains, bucketed by variant
+    sidx = list(by_state.keys())
+    buckets = OrderedDict()
+    first = 0
+    for si in sidx:
+        cnt = len(by_state[si])
+        buckets.setdefault(states[si].variant, []).append((si, first, cnt))
+        first += cnt
+    d_pt = DeviceBuffer(pt_total)
+    d_wire = DeviceBuffer(wire_total)
+    d_recs = DeviceBuffer(ctypes.sizeof(recs))
+    d_len = DeviceBuffer(4 * nrec)
+    d_states = DeviceBuffer(STATE_BYTES * len(states))
+    d_pt.upload(pt_host, stream=stream)
+    d_recs.upload(np.frombuffer(recs, dtype=np.uint8), stream=stream)
+    d_states.upload(pack_states(states), stream=stream)
+    d_wire.zero(stream)
+    chain_bufs = []
+    for var, chs in buckets.items():
+        c = make_chains([x[0] for x in chs], [x[1] for x in chs], [x[2] for x in chs])
+        d_ch = DeviceBuffer(ctypes.sizeof(c))
+        d_ch.upload(np.frombuffer(c, dtype=np.uint8), stream=stream)
+        chain_bufs.append(d_ch)
+        seal_dev(d_ch, len(chs), d_recs, d_pt, d_wire, d_states, d_len, var, stream)
+    if stream is not None:
+        stream.synchronize()
+    wire_host = d_wire.download()
+    lens = d_len.download().view(np.int32)
+    unpack_states(d_states.download(), states)
+    synchronize()
+    out = [b""] * nrec
+    for k, i in enumerate(order):
+        L = int(lens[k])
+        if L < 0:
+            raise N.TLSGPUError(L, "seal record %d" % i)
+        if L != wlen[k]:
+            raise RuntimeError("wire length mismatch %d != %d" % (L, wlen[k]))
+        o = int(wire_off[k])
+        out[i] = wire_host[o:o + L].tobytes()
+    return out
+
+
+def seal_write(state, data, content_type=ContentType.application_data, fault=0):
+    """One TLSRecordLayer.write(): fragmentation + BEAST split + seal.
+    Returns the list of wire records in send order."""
+    payloads = plan_write(data, state.version, state.isBlockCipher)
+    return seal([state], [(0, p, content_type, fault) for p in payloads])
