@@ -1,0 +1,284 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json headline: device-resident AES-128-CBC + HMAC-SHA1
+TLS-record seal of 64 Ki x 16 KiB records (config 2), in plaintext GiB/s.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+A step = one seal of the whole per-GPU batch (every record MAC'd, padded,
+CBC-encrypted and framed; connection states carried from the previous step).
+Multi-GPU is weak scaling: each rank owns its own batch on its own device
+(connection sharding, no collective on the data path); torch.distributed (gloo)
+is only used for the start/stop barriers and the max-over-ranks time.
+
+Prints ONE JSON line (rank 0) with roofline + cpu_baseline objects.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
+    ap.add_argument("--records", type=int, default=None, help="override record count (debug)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline")
+    ap.add_argument("--no-check", action="store_true", help="skip the full-batch parity check")
+    ap.add_argument("--host-inclusive", action="store_true", default=True)
+    ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
+    return ap.parse_args()
+
+
+class Dist:
+    def __init__(self, n):
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist  # plumbing only: barrier + max
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x):
+        if not self.dist:
+            return x
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        return float(t.item())
+
+
+def build_workload(name, rank, world, records=None):
+    from tlslite_amd import workloads as W
+    if name == "cfg4":
+        kw = {} if records is None else {"nconn": records}
+        return W.cfg4(rank=rank, world=world, **kw)
+    kw = {} if records is None else {"n": records}
+    return W.CONFIGS[name](**kw)
+
+
+def oracle_check(wl, wire_gpu, nthreads, sample=None):
+    """Seal the same workload with the CPU oracle; returns (bit_exact, seconds,
+    records, plaintext bytes, threads)."""
+    from oracle import oracle as O
+    idx_chains = np.arange(wl.n_chains) if sample is None else sample
+    protos = []
+    for c in idx_chains:
+        g = wl.groups[wl.chain_group[c]]
+        gi = c - int(np.searchsorted(wl.chain_group, wl.chain_group[c]))
+        key = g.keys[gi % len(g.keys)]
+        mk = g.mac_keys[gi % len(g.mac_keys)]
+        fiv = g.fixed_ivs[gi % len(g.fixed_ivs)] if g.fixed_ivs is not None else None
+        iv = bytes(g.ivs[gi]) if g.ivs is not None else b""
+        protos.append(O.Conn.for_suite(g.suite, g.version, bytes(key), iv, bytes(mk),
+                                       None if fiv is None else bytes(fiv), int(g.seq0[gi])))
+    pt = O.fill_pattern(wl.pt_bytes, wl.seed)
+    wire = np.zeros(wl.wire_bytes, dtype=np.uint8)
+    t0 = time.perf_counter()
+    wl_len = O.seal_batch(protos, wl.chain_first[idx_chains], wl.chain_count[idx_chains], pt, wl.pt_off, wl.pt_len,
+                          wire, wl.wire_off, nthreads=nthreads)
+    dt = time.perf_counter() - t0
+    recs = np.concatenate([np.arange(wl.chain_first[c], wl.chain_first[c] + wl.chain_count[c]) for c in idx_chains])
+    ok = True
+    for r in recs:
+        o, L = int(wl.wire_off[r]), int(wl.wire_len[r])
+        if int(wl_len[r]) != L:
+            ok = False
+            break
+    if ok:
+        mask = np.zeros(wl.wire_bytes, dtype=bool)
+        if sample is None:
+            ok = bool(np.array_equal(wire, wire_gpu))
+        else:
+            for r in recs:
+                o, L = int(wl.wire_off[r]), int(wl.wire_len[r])
+                if not np.array_equal(wire[o:o + L], wire_gpu[o:o + L]):
+                    ok = False
+                    break
+        del mask
+    return ok, dt, len(recs), int(wl.pt_len[recs].sum()), nthreads
+
+
+def host_inclusive_rate(wl, nsub=16):
+    """Plaintext GiB/s including pinned H2D of plaintext + seal + D2H of wire,
+    pipelined over `nsub` sub-batches on 3 streams (copies overlap kernels)."""
+    import ctypes
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import Event, PinnedBuffer, Stream, synchronize
+    if len(wl.launches) != 1:
+        return None
+    var, _, nch = wl.launches[0]
+    if nch != wl.n_records:  # only for one-record chains laid out in order
+        return None
+    from tlslite_amd.recordlayer import make_chains
+    from tlslite_amd.device import DeviceBuffer
+    pin_pt = PinnedBuffer(wl.pt_bytes)
+    pin_wire = PinnedBuffer(wl.wire_bytes)
+    wl.d_pt.download(out=pin_pt.array[: wl.pt_bytes])
+    streams = [Stream() for _ in range(3)]
+    per = (wl.n_records + nsub - 1) // nsub
+    subs = []
+    for s in range(nsub):
+        a, b = s * per, min(wl.n_records, (s + 1) * per)
+        if a >= b:
+            break
+        ch = make_chains(np.arange(a, b, dtype=np.uint32), np.arange(a, b, dtype=np.uint32),
+                         np.ones(b - a, dtype=np.uint32))
+        d = DeviceBuffer(ctypes.sizeof(ch))
+        d.upload(np.frombuffer(ch, dtype=np.uint8))
+        p0, p1 = int(wl.pt_off[a]), int(wl.pt_off[b - 1]) + int(wl.pt_len[b - 1])
+        w0, w1 = int(wl.wire_off[a]), int(wl.wire_off[b - 1]) + int(wl.wire_len[b - 1])
+        subs.append((d, b - a, p0, p1, w0, w1))
+    best = None
+    for _rep in range(3):
+        wl.reset_states()
+        synchronize()
+        t0 = time.perf_counter()
+        for i, (d, n, p0, p1, w0, w1) in enumerate(subs):
+            st = streams[i % 3]
+            N.call("tlsgpu_memcpy_h2d", wl.d_pt.at(p0), ctypes.c_void_p(pin_pt.ptr.value + p0), p1 - p0, st.handle)
+            N.call("tlsgpu_seal_dev", d.ptr, n, wl.d_recs.ptr, wl.d_pt.ptr, wl.d_wire.ptr, wl.d_states.ptr,
+                   wl.d_len.ptr, var, st.handle)
+            N.call("tlsgpu_memcpy_d2h", ctypes.c_void_p(pin_wire.ptr.value + w0 - 11), wl.d_wire.at(w0 - 11),
+                   w1 - w0 + 11, st.handle)
+        for st in streams:
+            st.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    rate = wl.plaintext_total / GIB / best
+    return {"value": round(rate, 2), "unit": "GiB/s", "ms": round(best * 1e3, 3),
+            "method": "pinned hipMemcpyAsync H2D(plaintext) + seal + D2H(wire), %d sub-batches on 3 streams" % len(subs)}
+
+
+def main():
+    args = parse()
+    D = Dist(args.gpus)
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import Event, Stream, set_device, synchronize, device_count, arch
+    if device_count() < 1:
+        raise SystemExit("bench.py: no GPU visible to libtlsgpu.so")
+    set_device(D.local % device_count())
+    wl = build_workload(args.config, D.rank, D.world, args.records)
+    stream = Stream()
+    wl.to_device(stream)
+    stream.synchronize()
+
+    # ---- parity of one launch against the CPU oracle (full batch, rank 0 at N=1)
+    bit_exact = None
+    cpu = None
+    if D.world == 1 and not args.no_check:
+        wl.launch([stream])
+        stream.synchronize()
+        wire_gpu = wl.d_wire.download()
+        nthreads = min(16, os.cpu_count() or 1)
+        ok, dt, nrec, ptb, th = oracle_check(wl, wire_gpu, nthreads)
+        bit_exact = ok
+        if not args.no_cpu:
+            cpu = {"value": round(ptb / GIB / dt, 4), "unit": "GiB/s", "cores": th, "kind": "port",
+                   "sample": "full batch (%d records, %.1f MiB plaintext) sealed by oracle/tls_oracle.c "
+                             "(C restatement of tlslite's _sendMsg path), %d pthreads, %.2f s"
+                             % (nrec, ptb / 2 ** 20, th, dt)}
+        wl.reset_states(stream)
+        stream.synchronize()
+
+    # ---- warmup + timed region
+    for _ in range(args.warmup):
+        wl.launch([stream])
+    synchronize()
+    D.barrier()
+    synchronize()
+    ev = [Event() for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for k in range(args.steps):
+        wl.launch([stream])
+        ev[k + 1].record(stream)
+    stream.synchronize()
+    synchronize()
+    wall = time.perf_counter() - t0
+    D.barrier()
+    per_launch = [ev[k].elapsed_ms(ev[k + 1]) for k in range(args.steps)]
+    gpu_ms = ev[0].elapsed_ms(ev[-1])
+    my_time = max(wall, gpu_ms / 1e3)
+    t_max = D.max(my_time)
+    total_pt = D.sum(wl.plaintext_total * args.steps)
+    value = total_pt / GIB / t_max
+
+    # roofline of the dominant kernel (the seal kernel is the only one in the step)
+    avg_ms = float(np.mean(per_launch))
+    alg_bytes = wl.plaintext_total + wl.wire_total  # read P + write 5+C per record
+    achieved = alg_bytes / (avg_ms / 1e3) / 1e9
+    traffic = None
+    tpath = args.traffic or os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.config)
+    if os.path.exists(tpath):
+        try:
+            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    host_inc = None
+    if D.world == 1 and args.host_inclusive:
+        try:
+            host_inc = host_inclusive_rate(wl)
+        except Exception as e:  # reported, never silently replaced
+            host_inc = {"error": str(e)}
+
+    if D.rank == 0:
+        out = {
+            "metric": "GiB/s device-resident AES-128-CBC+HMAC-SHA1 TLS-record encrypt, 16KiB records"
+            if args.config == "cfg2" else "GiB/s device-resident TLS-record seal (%s)" % args.config,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": D.world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 plaintext, seeded keys/IVs)",
+            "config": {"workload": wl.name, "records_per_gpu": wl.n_records,
+                       "plaintext_bytes_per_gpu": wl.plaintext_total,
+                       "parallelism": "connection-sharded x%d (no collective)" % D.world,
+                       "device": arch(D.local % device_count())},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_avg_ms": round(avg_ms, 4), "alg_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+            "bit_exact": bit_exact,
+            "host_inclusive": host_inc,
+        }
+        print(json.dumps(out))
+    if D.dist:
+        D.dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,231 @@
+"""Device-resident synthetic workloads for the BASELINE.json configs
+(SURVEY.md §8d).  A workload is plain data (keys, IVs, seqnums, offsets,
+plaintext seed) plus the HBM arenas built from it, so the same description
+can be replayed by a CPU checker.
+
+  cfg2  64 Ki x 16 KiB records, AES-128-CBC + HMAC-SHA1, TLS 1.2, one key /
+        MAC key / fixedIV, per-record CBC IV, seqnum = record index
+  cfg3  1 Mi x 1434 B records, AES-256-CBC + HMAC-SHA256, TLS 1.2, per-record IV
+  cfg4  C connections x R records, AES-128-CBC-SHA, per-connection keys,
+        records chained inside a connection (residue / seqnum carried)
+  cfg5  RC4-SHA and 3DES-EDE-CBC-SHA records interleaved 50/50 (seeded
+        shuffle), fresh connection per record, one launch per suite variant
+
+Plaintext bytes come from the device splitmix64 generator
+(tlsgpu_fill_pattern) with a per-config seed: byte i of the arena is byte
+(i & 7) of splitmix64(seed + (i >> 3)).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from .constants import ContentType, suite_primitives
+from .device import DeviceBuffer, fill_pattern
+from .recordlayer import make_chains, make_records
+from .state import STATE_BYTES, ConnectionState
+
+
+def _round_up(x, a):
+    return (x + a - 1) // a * a
+
+
+class Group:
+    """Connections of one suite in a workload."""
+
+    def __init__(self, suite, version, keys, ivs, mac_keys, fixed_ivs, seq0, recs_per_conn, pt_len):
+        self.suite, self.version = suite, tuple(version)
+        self.keys, self.ivs, self.mac_keys, self.fixed_ivs = keys, ivs, mac_keys, fixed_ivs
+        self.seq0 = np.asarray(seq0, dtype=np.uint64)
+        self.recs_per_conn, self.pt_len = int(recs_per_conn), int(pt_len)
+
+    @property
+    def nconn(self):
+        return len(self.seq0)
+
+
+class Workload:
+    """Host description + device arenas.  Record r of the flat descriptor
+    array belongs to chain chain_of[r]; chains of one variant are launched
+    together."""
+
+    def __init__(self, name, groups, seed, rec_order=None):
+        self.name, self.groups, self.seed = name, groups, seed
+        # flat records in chain order
+        states, pt_len, chain_first, chain_count, chain_group = [], [], [], [], []
+        r = 0
+        for gi, g in enumerate(groups):
+            for c in range(g.nconn):
+                chain_first.append(r)
+                chain_count.append(g.recs_per_conn)
+                chain_group.append(gi)
+                pt_len += [g.pt_len] * g.recs_per_conn
+                r += g.recs_per_conn
+        self.n_records = r
+        self.n_chains = len(chain_first)
+        self.pt_len = np.asarray(pt_len, dtype=np.uint32)
+        self.chain_first = np.asarray(chain_first, dtype=np.uint32)
+        self.chain_count = np.asarray(chain_count, dtype=np.uint32)
+        self.chain_group = np.asarray(chain_group, dtype=np.int32)
+        # arena placement: rec_order permutes records in memory (cfg5 interleave)
+        order = np.arange(r) if rec_order is None else np.asarray(rec_order)
+        self.slot_of = np.empty(r, dtype=np.int64)
+        self.slot_of[order] = np.arange(r)
+        pt_stride = np.array([_round_up(int(x), 16) for x in self.pt_len])
+        wlen = np.array([self._wire_len(g, int(n)) for g, n in self._rec_groups()], dtype=np.int64)
+        self.wire_len = wlen
+        wire_stride = np.array([_round_up(int(w), 16) for w in wlen])
+        # offsets in slot order
+        ps = pt_stride[order]
+        ws = wire_stride[order]
+        pt_off_slot = np.concatenate([[0], np.cumsum(ps)[:-1]])
+        wire_off_slot = np.concatenate([[0], np.cumsum(ws)[:-1]]) + 11
+        self.pt_off = pt_off_slot[self.slot_of].astype(np.uint64)
+        self.wire_off = wire_off_slot[self.slot_of].astype(np.uint64)
+        self.pt_bytes = int(ps.sum())
+        self.wire_bytes = int(ws.sum()) + 16
+        self.plaintext_total = int(self.pt_len.sum())
+        self.wire_total = int(wlen.sum())
+
+    def _rec_groups(self):
+        for gi, g in enumerate(self.groups):
+            for _ in range(g.nconn * g.recs_per_conn):
+                yield g, g.pt_len
+
+    @staticmethod
+    def _wire_len(g, n):
+        cipher, mac, _, _, ml = suite_primitives(g.suite)
+        if n == 0:
+            return 0
+        if cipher == "rc4":
+            return 5 + n + ml
+        bs = 8 if cipher == "3des" else 16
+        e = bs if g.version >= (3, 2) else 0
+        cur = e + n + ml
+        return 5 + cur + (bs - cur % bs)
+
+    # ------------------------------------------------------------ host states
+    def host_states(self):
+        """numpy uint8 [n_chains * 2048] of initial connection states."""
+        out = np.zeros(self.n_chains * STATE_BYTES, dtype=np.uint8)
+        ci = 0
+        for g in self.groups:
+            proto_cache = {}
+            for c in range(g.nconn):
+                k = g.keys[c % len(g.keys)]
+                mk = g.mac_keys[c % len(g.mac_keys)]
+                fiv = g.fixed_ivs[c % len(g.fixed_ivs)] if g.fixed_ivs is not None else None
+                key = (bytes(k), bytes(mk), None if fiv is None else bytes(fiv))
+                if key not in proto_cache:
+                    iv0 = bytes(g.ivs[c]) if g.ivs is not None else b""
+                    proto_cache[key] = ConnectionState.for_suite(g.suite, g.version, key[0], iv0, key[1], key[2], 0)
+                st = proto_cache[key]
+                blob = out[ci * STATE_BYTES:(ci + 1) * STATE_BYTES]
+                blob[:] = np.frombuffer(st.raw, dtype=np.uint8)
+                p = (ctypes.c_uint8 * STATE_BYTES).from_buffer(blob)
+                if g.ivs is not None and len(g.ivs[c]):
+                    N.call("tlsgpu_conn_state_set_iv", p, ctypes.c_char_p(bytes(g.ivs[c])), len(g.ivs[c]))
+                N.call("tlsgpu_conn_state_set_seqnum", p, int(g.seq0[c]))
+                ci += 1
+        return out
+
+    # ------------------------------------------------------------ device arenas
+    def to_device(self, stream=None, fill=True):
+        self.d_pt = DeviceBuffer(self.pt_bytes)
+        self.d_wire = DeviceBuffer(self.wire_bytes)
+        self.d_len = DeviceBuffer(4 * self.n_records)
+        recs = make_records(self.pt_off, self.wire_off, self.pt_len, ContentType.application_data, 0)
+        self.d_recs = DeviceBuffer(ctypes.sizeof(recs))
+        self.d_recs.upload(np.frombuffer(recs, dtype=np.uint8))
+        st = self.host_states()
+        self.d_states = DeviceBuffer(st.nbytes)
+        self.d_states0 = DeviceBuffer(st.nbytes)
+        self.d_states0.upload(st)
+        self.d_states.upload(st)
+        # one chain array per variant
+        self.launches = []
+        var_of_group = [ConnectionState.for_suite(
+            g.suite, g.version, bytes(g.keys[0]), bytes(g.ivs[0]) if g.ivs is not None else b"",
+            bytes(g.mac_keys[0]), bytes(g.fixed_ivs[0]) if g.fixed_ivs is not None else None).variant
+            for g in self.groups]
+        for var in sorted(set(var_of_group)):
+            idx = [c for c in range(self.n_chains) if var_of_group[self.chain_group[c]] == var]
+            ch = make_chains(np.asarray(idx, dtype=np.uint32), self.chain_first[idx], self.chain_count[idx])
+            d = DeviceBuffer(ctypes.sizeof(ch))
+            d.upload(np.frombuffer(ch, dtype=np.uint8))
+            self.launches.append((var, d, len(idx)))
+        if fill:
+            fill_pattern(self.d_pt, self.pt_bytes, self.seed, 0, 0, stream)
+        self.d_wire.zero(stream)
+        return self
+
+    def reset_states(self, stream=None):
+        N.call("tlsgpu_memcpy_d2d", self.d_states.ptr, self.d_states0.ptr, self.d_states.nbytes,
+               stream.handle if stream else None)
+
+    def launch(self, streams=None):
+        """Seal every record once (one kernel launch per suite variant; with
+        several streams the variants run concurrently)."""
+        for i, (var, d_ch, nch) in enumerate(self.launches):
+            s = None if not streams else streams[i % len(streams)]
+            N.call("tlsgpu_seal_dev", d_ch.ptr, nch, self.d_recs.ptr, self.d_pt.ptr, self.d_wire.ptr,
+                   self.d_states.ptr, self.d_len.ptr, var, s.handle if s else None)
+
+    def free(self):
+        for name in ("d_pt", "d_wire", "d_len", "d_recs", "d_states", "d_states0"):
+            b = getattr(self, name, None)
+            if b is not None:
+                b.free()
+        for _, d, _ in getattr(self, "launches", []):
+            d.free()
+
+
+def _rng_bytes(rng, n, k):
+    return [rng.bytes(k) for _ in range(n)]
+
+
+def cfg2(n=65536, pt_len=16384, seed=2):
+    rng = np.random.default_rng(seed)
+    key, mk, fiv = rng.bytes(16), rng.bytes(20), rng.bytes(16)
+    ivs = np.frombuffer(rng.bytes(16 * n), dtype=np.uint8).reshape(n, 16)
+    g = Group("AES128-SHA", (3, 3), [key], ivs, [mk], [fiv], np.arange(n, dtype=np.uint64), 1, pt_len)
+    return Workload("cfg2: %d x %d B records, TLS_RSA_WITH_AES_128_CBC_SHA, TLS 1.2, per-record IV" % (n, pt_len),
+                    [g], seed)
+
+
+def cfg3(n=1048576, pt_len=1434, seed=3):
+    rng = np.random.default_rng(seed)
+    key, mk, fiv = rng.bytes(32), rng.bytes(32), rng.bytes(16)
+    ivs = np.frombuffer(rng.bytes(16 * n), dtype=np.uint8).reshape(n, 16)
+    g = Group("AES256-SHA256", (3, 3), [key], ivs, [mk], [fiv], np.arange(n, dtype=np.uint64), 1, pt_len)
+    return Workload("cfg3: %d x %d B records, TLS_RSA_WITH_AES_256_CBC_SHA256, TLS 1.2" % (n, pt_len), [g], seed)
+
+
+def cfg4(nconn=4096, recs_per_conn=256, pt_len=16384, seed=4, rank=0, world=1):
+    """Connection-sharded: this rank owns connections [rank::world]."""
+    rng = np.random.default_rng(seed)
+    keys = _rng_bytes(rng, nconn, 16)
+    mks = _rng_bytes(rng, nconn, 20)
+    fivs = _rng_bytes(rng, nconn, 16)
+    ivs = np.frombuffer(rng.bytes(16 * nconn), dtype=np.uint8).reshape(nconn, 16)
+    mine = np.arange(rank, nconn, world)
+    g = Group("AES128-SHA", (3, 3), [keys[i] for i in mine], ivs[mine], [mks[i] for i in mine],
+              [fivs[i] for i in mine], np.zeros(len(mine), dtype=np.uint64), recs_per_conn, pt_len)
+    return Workload("cfg4: %d conns x %d records of %d B, AES128-SHA, chained (rank %d/%d)"
+                    % (nconn, recs_per_conn, pt_len, rank, world), [g], seed + 1000 * rank)
+
+
+def cfg5(n=65536, pt_len=16384, seed=5):
+    rng = np.random.default_rng(seed)
+    half = n // 2
+    k_rc4, mk1 = rng.bytes(16), rng.bytes(20)
+    k_des, mk2, fiv = rng.bytes(24), rng.bytes(20), rng.bytes(8)
+    ivs = np.frombuffer(rng.bytes(8 * (n - half)), dtype=np.uint8).reshape(n - half, 8)
+    g1 = Group("RC4-SHA", (3, 3), [k_rc4], None, [mk1], None, np.arange(half, dtype=np.uint64), 1, pt_len)
+    g2 = Group("3DES-SHA", (3, 3), [k_des], ivs, [mk2], [fiv], np.arange(half, n, dtype=np.uint64), 1, pt_len)
+    order = rng.permutation(n)  # interleave the two suites in the arenas
+    return Workload("cfg5: %d x %d B records, RC4-SHA / 3DES-EDE-CBC-SHA interleaved" % (n, pt_len), [g1, g2], seed,
+                    rec_order=order)
+
+
+CONFIGS = {"cfg2": cfg2, "cfg3": cfg3, "cfg4": cfg4, "cfg5": cfg5}
