@@ -109,18 +109,23 @@ __device__ __forceinline__ void load_partial(const uint8_t* p, uint32_t r, uint3
 constexpr uint32_t AES_LDS_BYTES = 131072;
 constexpr uint32_t AES_DEC_LDS_BYTES = 131072 + 32768;  // + inverse S-box (32 copies)
 
+// lds == nullptr: the caller addresses dynamic LDS from byte 0 (no extern symbol)
 __device__ __forceinline__ void aes_lds_fill(uint32_t* lds, bool dec) {
+    typedef __attribute__((address_space(3))) uint32_t l3_t;
     for (uint32_t idx = threadIdx.x; idx < 32768; idx += blockDim.x) {
         uint32_t t = idx >> 13, e = (idx >> 5) & 255, c = idx & 31;
         uint32_t v = dec ? c_aes.td0[e] : c_aes.te0[e];
         v = (v << (8 * t)) | (t ? (v >> (32 - 8 * t)) : 0u);
         uint32_t byte = (t & 1) * 128 + (t >> 1) * 65536 + e * 256 + c * 4;
-        lds[byte >> 2] = v;
+        if (lds) lds[byte >> 2] = v;
+        else *(l3_t*)(size_t)byte = v;
     }
     if (dec) {
         for (uint32_t idx = threadIdx.x; idx < 8192; idx += blockDim.x) {
             uint32_t e = idx >> 5, c = idx & 31;
-            lds[(131072 + e * 128 + c * 4) >> 2] = c_aes.inv_sbox[e];
+            uint32_t byte = 131072 + e * 128 + c * 4;
+            if (lds) lds[byte >> 2] = c_aes.inv_sbox[e];
+            else *(l3_t*)(size_t)byte = c_aes.inv_sbox[e];
         }
     }
 }

@@ -12,6 +12,21 @@ namespace tg {
 TG_HD uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 TG_HD uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
+// 3-input boolean functions: one v_bitop3_b32 on gfx950 (truth table indexed
+// by a<<2 | b<<1 | c), plain C on the host.
+#ifdef __HIP_DEVICE_COMPILE__
+#define TG_BOP3(a, b, c, tt) __builtin_amdgcn_bitop3_b32((a), (b), (c), (tt))
+TG_HD uint32_t bx3(uint32_t a, uint32_t b, uint32_t c) { return TG_BOP3(a, b, c, 0x96); }        // a^b^c
+TG_HD uint32_t bch(uint32_t a, uint32_t b, uint32_t c) { return TG_BOP3(a, b, c, 0xCA); }        // a?b:c
+TG_HD uint32_t bmaj(uint32_t a, uint32_t b, uint32_t c) { return TG_BOP3(a, b, c, 0xE8); }       // majority
+TG_HD uint32_t bmd5i(uint32_t b, uint32_t c, uint32_t d) { return TG_BOP3(b, c, d, 0x39); }      // c^(b|~d)
+#else
+TG_HD uint32_t bx3(uint32_t a, uint32_t b, uint32_t c) { return a ^ b ^ c; }
+TG_HD uint32_t bch(uint32_t a, uint32_t b, uint32_t c) { return (a & b) | (~a & c); }
+TG_HD uint32_t bmaj(uint32_t a, uint32_t b, uint32_t c) { return (a & b) | (a & c) | (b & c); }
+TG_HD uint32_t bmd5i(uint32_t b, uint32_t c, uint32_t d) { return c ^ (b | ~d); }
+#endif
+
 template <int MAC>
 struct Hash;
 
@@ -30,21 +45,21 @@ struct Hash<TLSGPU_MAC_SHA1> {
             if (t < 16) {
                 wt = w[t];
             } else {
-                wt = rotl32(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+                wt = rotl32(bx3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
                 w[t & 15] = wt;
             }
             uint32_t f, k;
             if (t < 20) {
-                f = ((c ^ d) & b) ^ d;
+                f = bch(b, c, d);
                 k = 0x5A827999u;
             } else if (t < 40) {
-                f = b ^ c ^ d;
+                f = bx3(b, c, d);
                 k = 0x6ED9EBA1u;
             } else if (t < 60) {
-                f = (b & c) | ((b | c) & d);
+                f = bmaj(b, c, d);
                 k = 0x8F1BBCDCu;
             } else {
-                f = b ^ c ^ d;
+                f = bx3(b, c, d);
                 k = 0xCA62C1D6u;
             }
             uint32_t tmp = rotl32(a, 5) + f + e + k + wt;
@@ -86,16 +101,16 @@ struct Hash<TLSGPU_MAC_SHA256> {
                 wt = w[t];
             } else {
                 uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-                uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-                uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+                uint32_t s0 = bx3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+                uint32_t s1 = bx3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
                 wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
                 w[t & 15] = wt;
             }
-            uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-            uint32_t ch = ((f ^ g) & e) ^ g;
+            uint32_t S1 = bx3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+            uint32_t ch = bch(e, f, g);
             uint32_t t1 = hh + S1 + ch + Sha256K::K[t] + wt;
-            uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-            uint32_t mj = (a & b) | ((a | b) & c);
+            uint32_t S0 = bx3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+            uint32_t mj = bmaj(a, b, c);
             hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
         }
         h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
@@ -132,16 +147,16 @@ struct Hash<TLSGPU_MAC_MD5> {
             uint32_t f;
             int g;
             if (i < 16) {
-                f = ((c ^ d) & b) ^ d;
+                f = bch(b, c, d);
                 g = i;
             } else if (i < 32) {
-                f = ((b ^ c) & d) ^ c;
+                f = bch(d, b, c);
                 g = (5 * i + 1) & 15;
             } else if (i < 48) {
-                f = b ^ c ^ d;
+                f = bx3(b, c, d);
                 g = (3 * i + 5) & 15;
             } else {
-                f = c ^ (b | ~d);
+                f = bmd5i(b, c, d);
                 g = (7 * i) & 15;
             }
             uint32_t x = a + f + Md5K::K[i] + w[g];

@@ -4,7 +4,9 @@
 //   cipher_kernel  raw stateful CBC / RC4 encrypt+decrypt for the
 //                  cipher-object surface (python_aes.py:20-69, python_rc4.py:25-41)
 //   fill_kernel    deterministic synthetic input (splitmix64 byte stream)
+#include <stdlib.h>
 #include "tg_device.h"
+#include "tg_aesq.h"
 #include "tg_launch.h"
 
 namespace tg {
@@ -281,10 +283,47 @@ static hipError_t set_lds(K kern, uint32_t bytes) {
                                (int)bytes);
 }
 
+template <int NR, int MAC, bool SSL3>
+static hipError_t launch_seal_aesq(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                                   const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
+                                   hipStream_t s) {
+    auto kern = seal_aesq_kernel<NR, MAC, SSL3>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = set_lds(kern, Q_LDS_BYTES);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    dim3 grid((nchains + Q_CHAINS - 1) / Q_CHAINS);
+    static uint32_t skip = 0xffffffffu;
+    if (skip == 0xffffffffu) {  // TLSGPU_DEBUG_SKIP: 1 = no CBC bulk, 2 = no MAC bulk (timing ablation only)
+        const char* e = getenv("TLSGPU_DEBUG_SKIP");
+        skip = e ? (uint32_t)atoi(e) : 0u;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(Q_THREADS), Q_LDS_BYTES, s, chains, nchains, recs, pt, wire, states, wire_len,
+                       skip);
+    return hipGetLastError();
+}
+
+// TLSGPU_SEAL_IMPL=lane selects the one-lane-per-chain AES kernel (A/B only)
+static bool use_quad_aes() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TLSGPU_SEAL_IMPL");
+        v = (e && e[0] == 'l') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 template <class C, int MAC, bool SSL3>
 static hipError_t launch_seal_t(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                 const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
                                 hipStream_t s) {
+    if constexpr (CipherTraits<C>::ID == TLSGPU_CIPHER_AES128 || CipherTraits<C>::ID == TLSGPU_CIPHER_AES256) {
+        if (use_quad_aes())
+            return launch_seal_aesq<CipherTraits<C>::ID == TLSGPU_CIPHER_AES128 ? 10 : 14, MAC, SSL3>(
+                chains, nchains, recs, pt, wire, states, wire_len, s);
+    }
     auto kern = seal_kernel<C, MAC, SSL3>;
     constexpr uint32_t lds = CipherTraits<C>::LDS;
     static bool attr = false;
