@@ -45,7 +45,8 @@ enum {
     TLSGPU_CIPHER_AES128 = 1, /* aes128Suites: key 16, IV 16 */
     TLSGPU_CIPHER_AES256 = 2, /* aes256Suites: key 32, IV 16 */
     TLSGPU_CIPHER_RC4 = 3,    /* rc4Suites:    key 16, no IV */
-    TLSGPU_CIPHER_3DES = 4    /* tripleDESSuites: key 24, IV 8 */
+    TLSGPU_CIPHER_3DES = 4,   /* tripleDESSuites: key 24, IV 8 */
+    TLSGPU_CIPHER_AES192 = 5  /* no suite uses it; raw cipher objects only (aes.py:8 allows 24-byte keys) */
 };
 enum {
     TLSGPU_MAC_SHA1 = 1,   /* shaSuites, 20-byte MAC */

@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libtlsgpu.so")
 
 # constants mirrored from include/tlsgpu.h
-CIPHER_AES128, CIPHER_AES256, CIPHER_RC4, CIPHER_3DES = 1, 2, 3, 4
+CIPHER_AES128, CIPHER_AES256, CIPHER_RC4, CIPHER_3DES, CIPHER_AES192 = 1, 2, 3, 4, 5
 MAC_SHA1, MAC_SHA256, MAC_MD5 = 1, 2, 3
 FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
 OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH = 0, -1, -2, -3, -4, -5

@@ -38,6 +38,7 @@ CIPHERS = {
     "aes256": (N.CIPHER_AES256, 32, 16),
     "rc4": (N.CIPHER_RC4, 16, 0),
     "3des": (N.CIPHER_3DES, 24, 8),
+    "aes192": (N.CIPHER_AES192, 24, 16),  # cipher objects only
 }
 # MAC name -> (C-ABI id, MAC length)
 MACS = {"sha1": (N.MAC_SHA1, 20), "sha256": (N.MAC_SHA256, 32), "md5": (N.MAC_MD5, 16)}

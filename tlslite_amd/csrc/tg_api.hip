@@ -135,10 +135,12 @@ int cipher_setup(ConnState* st, int cipher, const uint8_t* key, size_t key_len, 
     st->cipher = (uint32_t)cipher;
     switch (cipher) {
         case TLSGPU_CIPHER_AES128:
+        case TLSGPU_CIPHER_AES192:
         case TLSGPU_CIPHER_AES256:
             // aes.py:8-13
-            if (key_len != (cipher == TLSGPU_CIPHER_AES128 ? 16u : 32u) || iv_len != 16 || !key || !iv)
-                return fail(TLSGPU_EINVAL, "AES needs a 16/32-byte key and a 16-byte IV");
+            if (key_len != (cipher == TLSGPU_CIPHER_AES128 ? 16u : cipher == TLSGPU_CIPHER_AES192 ? 24u : 32u) ||
+                iv_len != 16 || !key || !iv)
+                return fail(TLSGPU_EINVAL, "AES needs a 16/24/32-byte key and a 16-byte IV");
             aes_expand(st, key, (int)key_len);
             st->bs = 16;
             pack_le(st->iv, iv, 16);
@@ -280,6 +282,7 @@ int tlsgpu_conn_state_init(tlsgpu_conn_state* out, int cipher, int mac, int ver_
                            const uint8_t* mac_key, size_t mac_key_len, const uint8_t* fixed_iv,
                            size_t fixed_iv_len, uint64_t seqnum) {
     if (!out) return fail(TLSGPU_EINVAL, "null state");
+    if (cipher == TLSGPU_CIPHER_AES192) return fail(TLSGPU_EINVAL, "no TLS suite uses AES-192");
     memset(out, 0, sizeof *out);
     ConnState* st = S(out);
     if (ver_major != 3 || ver_minor < 0 || ver_minor > 3)
@@ -418,9 +421,16 @@ int tlsgpu_cipher_dev(const tlsgpu_span* spans, uint32_t nspans, const uint8_t* 
     return 0;
 }
 
-int tlsgpu_open_dev(const tlsgpu_chain*, uint32_t, const tlsgpu_open_record*, const uint8_t*, uint8_t*,
-                    tlsgpu_conn_state*, int32_t*, uint32_t, tlsgpu_stream) {
-    return fail(TLSGPU_EINVAL, "open path not built yet");
+int tlsgpu_open_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* records,
+                    const uint8_t* wire, uint8_t* pt, tlsgpu_conn_state* states, int32_t* status, uint32_t variant,
+                    tlsgpu_stream s) {
+    if (nchains == 0) return 0;
+    if (!chains || !records || !wire || !pt || !states || !status) return fail(TLSGPU_EINVAL, "null pointer");
+    bool known = false;
+    hipError_t e = launch_open(variant, chains, nchains, records, wire, pt, S(states), status, HS(s), &known);
+    if (!known) return fail(TLSGPU_EINVAL, "unsupported open variant");
+    if (e != hipSuccess) return fail_hip(e, "open launch");
+    return 0;
 }
 
 int tlsgpu_fill_pattern(uint8_t* dptr, size_t bytes, uint64_t seed, uint64_t start, tlsgpu_stream s) {

@@ -191,8 +191,9 @@ __global__ void __launch_bounds__(SEAL_BLOCK) cipher_kernel(const tlsgpu_span* _
                                                            const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                            ConnState* __restrict__ states) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    constexpr bool AES = CIPHER == TLSGPU_CIPHER_AES128 || CIPHER == TLSGPU_CIPHER_AES256;
-    constexpr int NR = CIPHER == TLSGPU_CIPHER_AES256 ? 14 : 10;
+    constexpr bool AES = CIPHER == TLSGPU_CIPHER_AES128 || CIPHER == TLSGPU_CIPHER_AES256 ||
+                         CIPHER == TLSGPU_CIPHER_AES192;
+    constexpr int NR = CIPHER == TLSGPU_CIPHER_AES256 ? 14 : CIPHER == TLSGPU_CIPHER_AES192 ? 12 : 10;
     if constexpr (AES) aes_lds_fill(lds, DEC);
     else if constexpr (CIPHER == TLSGPU_CIPHER_3DES) des_lds_fill(lds);
     __syncthreads();
@@ -249,6 +250,182 @@ __global__ void __launch_bounds__(SEAL_BLOCK) cipher_kernel(const tlsgpu_span* _
         for (uint32_t off = 0; off < sp.len; off++) dst[off] = (uint8_t)(src[off] ^ c.R.ks());
         c.save(st);
     }
+}
+
+// ---------------------------------------------------------------- record open
+// _decryptRecord (tlsrecordlayer.py:958-1044): decrypt (CBC residue / RC4
+// state carried), strip the TLS>=1.1 explicit IV, check padding, recompute and
+// compare the MAC.  One lane per chain; the plaintext (followed by the MAC
+// and padding bytes) is written at pt + pt_off.  status = plaintext length or
+// an alert code.  Two passes over the record: decrypt+store, then verify by
+// re-reading the lane's own stores.
+template <int NR>
+struct AesDecAdapter {
+    static constexpr int BS = 16;
+    AesCbcDec<NR> c;
+    __device__ __forceinline__ void load(const ConnState* st, const void* lds) { c.load(st, lds); }
+    __device__ __forceinline__ void save(ConnState* st) { c.save(st); }
+    __device__ __forceinline__ void dec_block(uint32_t* d) { c.dec_block(d); }
+};
+struct TdesDecAdapter {
+    static constexpr int BS = 8;
+    TdesCbc c;
+    __device__ __forceinline__ void load(const ConnState* st, const void* lds) { c.load(st, lds); }
+    __device__ __forceinline__ void save(ConnState* st) { c.save(st); }
+    __device__ __forceinline__ void dec_block(uint32_t* d) {
+        uint32_t c0 = d[0], c1 = d[1];
+        uint32_t hi = bswap32(d[0]), lo = bswap32(d[1]);
+        tdes_block<true>(hi, lo, c.ks, c.L);
+        d[0] = bswap32(hi) ^ c.iv[0];
+        d[1] = bswap32(lo) ^ c.iv[1];
+        c.iv[0] = c0;
+        c.iv[1] = c1;
+    }
+};
+
+template <int CIPHER>
+struct OpenTraits;
+template <> struct OpenTraits<TLSGPU_CIPHER_AES128> { using D = AesDecAdapter<10>; static constexpr uint32_t LDS = AES_DEC_LDS_BYTES; };
+template <> struct OpenTraits<TLSGPU_CIPHER_AES256> { using D = AesDecAdapter<14>; static constexpr uint32_t LDS = AES_DEC_LDS_BYTES; };
+template <> struct OpenTraits<TLSGPU_CIPHER_3DES> { using D = TdesDecAdapter; static constexpr uint32_t LDS = DES_LDS_BYTES; };
+template <> struct OpenTraits<TLSGPU_CIPHER_RC4> { using D = Rc4Stream; static constexpr uint32_t LDS = RC4_LDS_BYTES_PER_WAVE * (SEAL_BLOCK / 64); };
+
+template <int CIPHER, int MAC, bool SSL3>
+__global__ void __launch_bounds__(SEAL_BLOCK) open_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
+                                                         const tlsgpu_open_record* __restrict__ recs,
+                                                         const uint8_t* __restrict__ wire, uint8_t* __restrict__ pt,
+                                                         ConnState* __restrict__ states,
+                                                         int32_t* __restrict__ status) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr bool AES = CIPHER == TLSGPU_CIPHER_AES128 || CIPHER == TLSGPU_CIPHER_AES256;
+    constexpr bool STREAM = CIPHER == TLSGPU_CIPHER_RC4;
+    if constexpr (AES) aes_lds_fill(lds, true);
+    else if constexpr (CIPHER == TLSGPU_CIPHER_3DES) des_lds_fill(lds);
+    __syncthreads();
+    const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cid >= nchains) return;
+    const tlsgpu_chain ch = chains[cid];
+    ConnState* st = states + ch.state;
+    using M = RecMac<MAC, SSL3>;
+    constexpr int DL = M::DL;
+    if (st->cipher != (uint32_t)CIPHER || st->mac != (uint32_t)MAC || st->ssl3 != (SSL3 ? 1u : 0u) || st->raw) {
+        for (uint32_t k = 0; k < ch.count; k++) status[ch.first + k] = TLSGPU_EMISMATCH;
+        return;
+    }
+    typename OpenTraits<CIPHER>::D dc;
+    dc.load(st, lds);
+    uint64_t seq = st->seqnum;
+    for (uint32_t k = 0; k < ch.count; k++) {
+        const tlsgpu_open_record R = recs[ch.first + k];
+        const uint8_t* Cb = wire + R.ct_off;
+        uint8_t* Pb = pt + R.pt_off;
+        const uint32_t L = R.ct_len;
+        uint32_t len, totalPad = 0;
+        bool padGood = true;
+        if constexpr (!STREAM) {
+            constexpr uint32_t BS = OpenTraits<CIPHER>::D::BS;
+            const uint32_t E = st->explicit_iv ? BS : 0u;
+            if (L % BS) {  // :964-968
+                status[ch.first + k] = TLSGPU_ALERT_DECRYPTION_FAILED;
+                continue;
+            }
+            for (uint32_t off = 0; off < L; off += BS) {
+                uint32_t d[4];
+                if (BS == 16) load16(Cb + off, d); else load8(Cb + off, d);
+                dc.dec_block(d);
+                if (off >= E) {
+                    if (BS == 16) store16(Pb + off - E, d); else store8(Pb + off - E, d);
+                }
+            }
+            len = L - E;  // :970-971
+            if (len == 0) {  // :973-977
+                status[ch.first + k] = TLSGPU_ALERT_DECRYPTION_FAILED;
+                continue;
+            }
+            const uint32_t pl = Pb[len - 1];
+            if (pl + 1 > len) {  // :981-983
+                padGood = false;
+            } else {
+                totalPad = pl + 1;
+                if (!SSL3) {  // TLS: every padding byte must equal the length (:986-993)
+                    for (uint32_t i = len - totalPad; i < len - 1; i++)
+                        if (Pb[i] != pl) padGood = false;
+                    if (!padGood) totalPad = 0;
+                }
+            }
+        } else {
+            for (uint32_t i = 0; i < L; i++) Pb[i] = (uint8_t)(Cb[i] ^ dc.R.ks());
+            len = L;
+        }
+        bool macGood = true;
+        const uint32_t endLen = DL + totalPad;
+        uint32_t n = 0;
+        if (endLen > len) {  // :1006-1007
+            macGood = false;
+        } else {
+            n = len - endLen;
+            M mac;
+            mac.begin(st, seq, R.content_type, n);
+            const uint32_t nfull = n >> 6;
+            for (uint32_t c = 0; c < nfull; c++) {
+                uint32_t cur[16];
+                load64(Pb + 64 * c, cur);
+                mac.update(cur);
+            }
+            uint32_t tail[16];
+            load_partial(Pb + 64 * nfull, n & 63, tail);
+            uint32_t m[8];
+            mac.finish(tail, (int)(n & 63), n, st, m);
+            seq++;  // getSeqNumBytes (:1018) runs whenever the MAC is computed
+#pragma unroll
+            for (int i = 0; i < DL; i++)
+                if (Pb[n + i] != (uint8_t)(m[i >> 2] >> (8 * (i & 3)))) macGood = false;
+        }
+        status[ch.first + k] = (padGood && macGood) ? (int32_t)n : TLSGPU_ALERT_BAD_RECORD_MAC;
+    }
+    st->seqnum = seq;
+    dc.save(st);
+}
+
+template <int CIPHER, int MAC, bool SSL3>
+static hipError_t launch_open_t(const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
+                                const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s) {
+    auto kern = open_kernel<CIPHER, MAC, SSL3>;
+    constexpr uint32_t lds = OpenTraits<CIPHER>::LDS;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    dim3 grid((n + SEAL_BLOCK - 1) / SEAL_BLOCK);
+    hipLaunchKernelGGL(kern, grid, dim3(SEAL_BLOCK), lds, s, chains, n, recs, wire, pt, states, status);
+    return hipGetLastError();
+}
+
+hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
+                       const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s,
+                       bool* known) {
+    *known = true;
+#define TG_OPEN_CASE(CIPHER_ID, MAC_ID, SSL3)                                                  \
+    if (variant == TLSGPU_VARIANT(CIPHER_ID, MAC_ID, SSL3))                                    \
+        return launch_open_t<CIPHER_ID, MAC_ID, SSL3>(chains, n, recs, wire, pt, states, status, s);
+    TG_OPEN_CASE(TLSGPU_CIPHER_AES128, TLSGPU_MAC_SHA1, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_AES256, TLSGPU_MAC_SHA1, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_AES128, TLSGPU_MAC_SHA256, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_AES256, TLSGPU_MAC_SHA256, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_3DES, TLSGPU_MAC_SHA1, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_SHA1, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_MD5, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_AES128, TLSGPU_MAC_SHA1, true)
+    TG_OPEN_CASE(TLSGPU_CIPHER_AES256, TLSGPU_MAC_SHA1, true)
+    TG_OPEN_CASE(TLSGPU_CIPHER_3DES, TLSGPU_MAC_SHA1, true)
+    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_SHA1, true)
+    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_MD5, true)
+#undef TG_OPEN_CASE
+    *known = false;
+    return hipSuccess;
 }
 
 // ---------------------------------------------------------------- synthetic input
@@ -367,7 +544,8 @@ template <int CIPHER, bool DEC>
 static hipError_t launch_cipher_t(const tlsgpu_span* spans, uint32_t n, const uint8_t* in, uint8_t* out,
                                   ConnState* states, hipStream_t s) {
     auto kern = cipher_kernel<CIPHER, DEC>;
-    constexpr bool AES = CIPHER == TLSGPU_CIPHER_AES128 || CIPHER == TLSGPU_CIPHER_AES256;
+    constexpr bool AES = CIPHER == TLSGPU_CIPHER_AES128 || CIPHER == TLSGPU_CIPHER_AES256 ||
+                         CIPHER == TLSGPU_CIPHER_AES192;
     constexpr uint32_t lds = AES ? (DEC ? AES_DEC_LDS_BYTES : AES_LDS_BYTES)
                                  : CIPHER == TLSGPU_CIPHER_3DES ? DES_LDS_BYTES
                                                                 : RC4_LDS_BYTES_PER_WAVE * (SEAL_BLOCK / 64);
@@ -391,6 +569,7 @@ hipError_t launch_cipher(int cipher, int dec, const tlsgpu_span* spans, uint32_t
                    : launch_cipher_t<ID, false>(spans, n, in, out, states, s);
     TG_CIPHER_CASE(TLSGPU_CIPHER_AES128)
     TG_CIPHER_CASE(TLSGPU_CIPHER_AES256)
+    TG_CIPHER_CASE(TLSGPU_CIPHER_AES192)
     TG_CIPHER_CASE(TLSGPU_CIPHER_3DES)
     TG_CIPHER_CASE(TLSGPU_CIPHER_RC4)
 #undef TG_CIPHER_CASE

@@ -12,6 +12,9 @@ hipError_t launch_seal(uint32_t variant, const tlsgpu_chain* chains, uint32_t nc
                        bool* known);
 hipError_t launch_cipher(int cipher, int dec, const tlsgpu_span* spans, uint32_t n, const uint8_t* in, uint8_t* out,
                          ConnState* states, hipStream_t s, bool* known);
+hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
+                       const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s,
+                       bool* known);
 hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, hipStream_t s);
 
 }  // namespace tg

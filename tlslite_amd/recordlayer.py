@@ -21,6 +21,39 @@ from .state import STATE_BYTES, pack_states, unpack_states
 PT_ALIGN = 16
 WIRE_BODY_ALIGN = 16  # record bodies start 16-byte aligned: wire_off % 16 == 11
 MAX_FRAGMENT = 16384  # tlsrecordlayer.py:273
+MAX_RECORD_BODY = 18432  # tlsrecordlayer.py:871 (16384 + 2048): record_overflow above
+
+
+class RecordOverflow(ValueError):
+    """A record header announced more than 18432 body bytes (record_overflow)."""
+
+
+class BadRecordMAC(ValueError):
+    """bad_record_mac alert (tlsrecordlayer.py:1039-1042)."""
+
+
+class DecryptionFailed(ValueError):
+    """decryption_failed alert (tlsrecordlayer.py:964-977)."""
+
+
+def parse_records(data):
+    """Split a received byte stream into (content_type, (major, minor), body)
+    records, RecordHeader3.parse style (messages.py:44-49).  Returns
+    (records, leftover_bytes) -- an incomplete trailing record stays in the
+    leftover."""
+    out = []
+    pos = 0
+    data = bytes(data)
+    while len(data) - pos >= 5:
+        ctype, vmaj, vmin = data[pos], data[pos + 1], data[pos + 2]
+        length = (data[pos + 3] << 8) | data[pos + 4]
+        if length > MAX_RECORD_BODY:
+            raise RecordOverflow("record length %d > %d" % (length, MAX_RECORD_BODY))
+        if len(data) - pos - 5 < length:
+            break
+        out.append((ctype, (vmaj, vmin), data[pos + 5:pos + 5 + length]))
+        pos += 5 + length
+    return out, data[pos:]
 
 
 def plan_write(data, version, block_cipher, max_fragment=MAX_FRAGMENT):
@@ -173,6 +206,109 @@ def seal(states, records, stream=None):
         o = int(wire_off[k])
         out[i] = wire_host[o:o + L].tobytes()
     return out
+
+
+def make_open_records(ct_off, pt_off, ct_len, content_type):
+    n = len(ct_len)
+    recs = (N.OpenRecord * n)()
+    a = np.frombuffer(recs, dtype=np.uint8).reshape(n, 24)
+    a[:, 0:8] = np.asarray(ct_off, dtype=np.uint64).reshape(n, 1).view(np.uint8)
+    a[:, 8:16] = np.asarray(pt_off, dtype=np.uint64).reshape(n, 1).view(np.uint8)
+    a[:, 16:20] = np.asarray(ct_len, dtype=np.uint32).reshape(n, 1).view(np.uint8)
+    a[:, 20] = np.broadcast_to(np.asarray(content_type, dtype=np.uint8), (n,))
+    a[:, 21:24] = 0
+    return recs
+
+
+def open_dev(chains, nchains, records, wire, pt, states, status, variant, stream=None):
+    """Device-resident batch open (decrypt + padding + MAC check)."""
+    def p(x):
+        return x.ptr if isinstance(x, DeviceBuffer) else ctypes.c_void_p(x)
+    N.call("tlsgpu_open_dev", p(chains), nchains, p(records), p(wire), p(pt), p(states), p(status), variant,
+           stream.handle if stream is not None else None)
+
+
+def open_records(states, records, stream=None):
+    """Open (decrypt + verify) records on the GPU -- the batched counterpart of
+    _decryptRecord (tlsrecordlayer.py:958-1044).
+
+    states:  list of read-direction ConnectionState (updated in place)
+    records: list of (state_index, content_type, body); records of one state
+             are opened in list order.
+    Returns a list of (status, plaintext): status 0 and the plaintext bytes,
+    or an alert code (N.ALERT_BAD_RECORD_MAC / N.ALERT_DECRYPTION_FAILED) and None.
+    """
+    nrec = len(records)
+    if nrec == 0:
+        return []
+    by_state = OrderedDict()
+    for i, r in enumerate(records):
+        by_state.setdefault(r[0], []).append(i)
+    order = [i for idxs in by_state.values() for i in idxs]
+    ct_off = np.zeros(nrec, dtype=np.uint64)
+    pos = 0
+    for k, i in enumerate(order):
+        ct_off[k] = pos
+        pos += len(records[i][2])
+        pos += (-pos) % PT_ALIGN
+    total = max(pos, 16)
+    host = np.zeros(total, dtype=np.uint8)
+    for k, i in enumerate(order):
+        b = bytes(records[i][2])
+        if b:
+            host[int(ct_off[k]):int(ct_off[k]) + len(b)] = np.frombuffer(b, dtype=np.uint8)
+    recs = make_open_records(ct_off, ct_off, [len(records[i][2]) for i in order], [records[i][1] for i in order])
+    buckets = OrderedDict()
+    first = 0
+    for si, idxs in by_state.items():
+        buckets.setdefault(states[si].variant, []).append((si, first, len(idxs)))
+        first += len(idxs)
+    d_ct = DeviceBuffer(total)
+    d_pt = DeviceBuffer(total)
+    d_recs = DeviceBuffer(ctypes.sizeof(recs))
+    d_st = DeviceBuffer(4 * nrec)
+    d_states = DeviceBuffer(STATE_BYTES * len(states))
+    d_ct.upload(host, stream=stream)
+    d_recs.upload(np.frombuffer(recs, dtype=np.uint8), stream=stream)
+    d_states.upload(pack_states(states), stream=stream)
+    d_pt.zero(stream)
+    keep = []
+    for var, chs in buckets.items():
+        c = make_chains([x[0] for x in chs], [x[1] for x in chs], [x[2] for x in chs])
+        d_ch = DeviceBuffer(ctypes.sizeof(c))
+        d_ch.upload(np.frombuffer(c, dtype=np.uint8), stream=stream)
+        keep.append(d_ch)
+        open_dev(d_ch, len(chs), d_recs, d_ct, d_pt, d_states, d_st, var, stream)
+    if stream is not None:
+        stream.synchronize()
+    pt_host = d_pt.download()
+    status = d_st.download().view(np.int32)
+    unpack_states(d_states.download(), states)
+    synchronize()
+    out = [None] * nrec
+    for k, i in enumerate(order):
+        st = int(status[k])
+        if st < 0:
+            out[i] = (st, None)
+        else:
+            o = int(ct_off[k])
+            out[i] = (0, pt_host[o:o + st].tobytes())
+    return out
+
+
+def open_stream(state, data):
+    """Parse + open every complete record of one connection's byte stream.
+    Raises BadRecordMAC / DecryptionFailed like the reference's alerts."""
+    recs, rest = parse_records(data)
+    res = open_records([state], [(0, ct, body) for ct, _, body in recs])
+    out = []
+    for (ct, _, _), (st, p) in zip(recs, res):
+        if st == N.ALERT_BAD_RECORD_MAC:
+            raise BadRecordMAC("MAC failure (or padding failure)")
+        if st == N.ALERT_DECRYPTION_FAILED:
+            raise DecryptionFailed("Encrypted data not a multiple of blocksize")
+        out.append((ct, p))
+    return out, rest
 
 
 def seal_write(state, data, content_type=ContentType.application_data, fault=0):
