@@ -42,38 +42,6 @@ def parse():
     return ap.parse_args()
 
 
-class Dist:
-    def __init__(self, n):
-        self.rank = int(os.environ.get("RANK", "0"))
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.dist = None
-        if self.world > 1:
-            import torch.distributed as dist  # plumbing only: barrier + max
-            dist.init_process_group("gloo")
-            self.dist = dist
-
-    def barrier(self):
-        if self.dist:
-            self.dist.barrier()
-
-    def max(self, x):
-        if not self.dist:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
-
-    def sum(self, x):
-        if not self.dist:
-            return x
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
-        return float(t.item())
-
-
 def build_workload(name, rank, world, records=None):
     from tlslite_amd import workloads as W
     if name == "cfg4":
@@ -98,7 +66,7 @@ def oracle_check(wl, wire_gpu, nthreads, sample=None):
         iv = bytes(g.ivs[gi]) if g.ivs is not None else b""
         protos.append(O.Conn.for_suite(g.suite, g.version, bytes(key), iv, bytes(mk),
                                        None if fiv is None else bytes(fiv), int(g.seq0[gi])))
-    pt = O.fill_pattern(wl.pt_bytes, wl.seed)
+    pt = wl.host_plaintext(O.fill_pattern)
     wire = np.zeros(wl.wire_bytes, dtype=np.uint8)
     t0 = time.perf_counter()
     wl_len = O.seal_batch(protos, wl.chain_first[idx_chains], wl.chain_count[idx_chains], pt, wl.pt_off, wl.pt_len,
@@ -178,7 +146,8 @@ def host_inclusive_rate(wl, nsub=16):
 
 def main():
     args = parse()
-    D = Dist(args.gpus)
+    from tlslite_amd.shard import ShardGroup
+    D = ShardGroup("gloo")
     from tlslite_amd import _native as N
     from tlslite_amd.device import Event, Stream, set_device, synchronize, device_count, arch
     if device_count() < 1:
@@ -276,8 +245,7 @@ def main():
             "host_inclusive": host_inc,
         }
         print(json.dumps(out))
-    if D.dist:
-        D.dist.destroy_process_group()
+    D.close()
 
 
 if __name__ == "__main__":

@@ -47,7 +47,8 @@ from tlslite.messages import ApplicationData  # noqa: E402
 from tlslite.mathtls import createHMAC, createMAC_SSL  # noqa: E402
 from tlslite.utils.cipherfactory import createAES, createRC4  # noqa: E402
 from tlslite.utils.tripledes import TripleDES  # noqa: E402
-from tlslite.constants import Fault  # noqa: E402
+from tlslite.constants import Fault, CipherSuite  # noqa: E402
+from tlslite.mathtls import PRF, PRF_1_2, PRF_SSL, calcMasterSecret  # noqa: E402
 
 
 def gen_bytes(seed, n):
@@ -298,6 +299,35 @@ def main():
     # (v) open-side vectors: decrypt+verify via _decryptRecord (:958-1044) of the
     #     sealed records in (iii) are covered by round trips; here record the alert
     #     the reference raises for tampered records.
+    # (vi) key-block derivation as _calcPendingStates does it (tlsrecordlayer.py:1097-1126):
+    #      master secret (mathtls.py:70-82) -> PRF/PRF_1_2/PRF_SSL key block -> slices
+    suite_ids = {"AES128-SHA": CipherSuite.TLS_RSA_WITH_AES_128_CBC_SHA,
+                 "AES256-SHA": CipherSuite.TLS_RSA_WITH_AES_256_CBC_SHA,
+                 "AES128-SHA256": CipherSuite.TLS_RSA_WITH_AES_128_CBC_SHA256,
+                 "RC4-SHA": CipherSuite.TLS_RSA_WITH_RC4_128_SHA,
+                 "RC4-MD5": CipherSuite.TLS_RSA_WITH_RC4_128_MD5,
+                 "3DES-SHA": CipherSuite.TLS_RSA_WITH_3DES_EDE_CBC_SHA}
+    for suite, sid in suite_ids.items():
+        for ver in VERSIONS:
+            if not valid(suite, ver):
+                continue
+            tag = "keys/%s/%d.%d" % (suite, ver[0], ver[1])
+            pms = bytearray(gen_bytes(tag + "/pms", 48))
+            cr = bytearray(gen_bytes(tag + "/cr", 32))
+            sr = bytearray(gen_bytes(tag + "/sr", 32))
+            ms = calcMasterSecret(ver, pms, cr, sr)
+            cipher, kl, ivl, mac, ml = SUITES[suite]
+            n = 2 * (ml + kl + ivl)
+            if ver == (3, 0):
+                kb = PRF_SSL(ms, sr + cr, n)
+            elif ver in ((3, 1), (3, 2)):
+                kb = PRF(ms, b"key expansion", sr + cr, n)
+            else:
+                kb = PRF_1_2(ms, b"key expansion", sr + cr, n)
+            cases.append({"kind": "keys", "name": tag, "suite": suite, "suite_id": sid, "version": list(ver),
+                          "premaster": bytes(pms).hex(), "client_random": bytes(cr).hex(),
+                          "server_random": bytes(sr).hex(), "master": bytes(ms).hex(), "key_block": bytes(kb).hex(),
+                          "key": "", "iv": "", "mac_key": "", "fixed_iv": "", "seq": 0})
     doc = {"generator": "tests/golden/make_golden.py",
            "reference": "trevp/tlslite 0.4.9 at /root/reference (pure-Python path); "
                         "3DES cipher = OpenSSL 3 EVP_des_ede3_cbc",

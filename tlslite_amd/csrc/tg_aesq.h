@@ -116,7 +116,9 @@ template <int NR, int MAC, bool SSL3>
 __global__ void __launch_bounds__(Q_THREADS, 3)
 seal_aesq_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
                  const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire, ConnState* __restrict__ states,
-                 int32_t* __restrict__ wire_len, uint32_t debug_skip) {
+                 int32_t* __restrict__ wire_len, uint32_t cpw, uint32_t debug_skip) {
+    // cpw = chains per workgroup (<= 256): small batches are spread over all
+    // CUs instead of packing 256 chains into a handful of workgroups
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
     constexpr uint32_t CIPHER_ID = NR == 10 ? TLSGPU_CIPHER_AES128 : TLSGPU_CIPHER_AES256;
@@ -130,7 +132,8 @@ seal_aesq_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, cons
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const bool is_aes = wave < Q_AES_WAVES;
     const uint32_t q = lane & 3;
-    const uint32_t base = blockIdx.x * Q_CHAINS;
+    const uint32_t base = blockIdx.x * cpw;
+    const uint32_t half = (cpw + 1) >> 1;  // quad j carries chains j and j + half
 
     if (!is_aes) {
         // ================================================= MAC lanes
@@ -139,7 +142,7 @@ seal_aesq_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, cons
         tlsgpu_chain ch = {0, 0, 0, 0};
         ConnState* st = nullptr;
         bool ok = false;
-        if (cid < nchains) {
+        if (local < cpw && cid < nchains) {
             ch = chains[cid];
             st = states + ch.state;
             ok = st->cipher == CIPHER_ID && st->mac == (uint32_t)MAC && st->ssl3 == (SSL3 ? 1u : 0u) && !st->raw;
@@ -213,15 +216,15 @@ seal_aesq_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, cons
     // win issue arbitration; the MAC waves fill the remaining slots.
     __builtin_amdgcn_s_setprio(2);
     const uint32_t quad = wave * 16 + (lane >> 2);  // 0..127
-    const uint32_t lA = quad, lB = quad + 128;      // local chain ids
+    const uint32_t lA = quad, lB = quad + half;     // local chain ids
     tlsgpu_chain cA = {0, 0, 0, 0}, cB = {0, 0, 0, 0};
     ConnState *sA = nullptr, *sB = nullptr;
     bool okA = false, okB = false;
     auto chk = [&](ConnState* s) {
         return s->cipher == CIPHER_ID && s->mac == (uint32_t)MAC && s->ssl3 == (SSL3 ? 1u : 0u) && !s->raw;
     };
-    if (base + lA < nchains) { cA = chains[base + lA]; sA = states + cA.state; okA = chk(sA); }
-    if (base + lB < nchains) { cB = chains[base + lB]; sB = states + cB.state; okB = chk(sB); }
+    if (lA < half && base + lA < nchains) { cA = chains[base + lA]; sA = states + cA.state; okA = chk(sA); }
+    if (lB < cpw && base + lB < nchains) { cB = chains[base + lB]; sB = states + cB.state; okB = chk(sB); }
     __syncthreads();
     const uint32_t maxcount = lds_read32(MISC);
     QuadAes aes;

@@ -471,14 +471,23 @@ static hipError_t launch_seal_aesq(const tlsgpu_chain* chains, uint32_t nchains,
         if (e != hipSuccess) return e;
         attr = true;
     }
-    dim3 grid((nchains + Q_CHAINS - 1) / Q_CHAINS);
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (ncu <= 0) ncu = 256;
+    }
+    uint32_t cpw = (nchains + ncu - 1) / (uint32_t)ncu;
+    cpw = cpw < 1 ? 1 : (cpw > (uint32_t)Q_CHAINS ? (uint32_t)Q_CHAINS : cpw);
+    dim3 grid((nchains + cpw - 1) / cpw);
     static uint32_t skip = 0xffffffffu;
     if (skip == 0xffffffffu) {  // TLSGPU_DEBUG_SKIP: 1 = no CBC bulk, 2 = no MAC bulk (timing ablation only)
         const char* e = getenv("TLSGPU_DEBUG_SKIP");
         skip = e ? (uint32_t)atoi(e) : 0u;
     }
     hipLaunchKernelGGL(kern, grid, dim3(Q_THREADS), Q_LDS_BYTES, s, chains, nchains, recs, pt, wire, states, wire_len,
-                       skip);
+                       cpw, skip);
     return hipGetLastError();
 }
 

@@ -49,7 +49,7 @@ class Workload:
     array belongs to chain chain_of[r]; chains of one variant are launched
     together."""
 
-    def __init__(self, name, groups, seed, rec_order=None):
+    def __init__(self, name, groups, seed, rec_order=None, chain_stream_start=None):
         self.name, self.groups, self.seed = name, groups, seed
         # flat records in chain order
         states, pt_len, chain_first, chain_count, chain_group = [], [], [], [], []
@@ -86,6 +86,33 @@ class Workload:
         self.wire_bytes = int(ws.sum()) + 16
         self.plaintext_total = int(self.pt_len.sum())
         self.wire_total = int(wlen.sum())
+        # position of each chain's plaintext in the splitmix stream: by default
+        # the arena offset; sharded workloads pass the unsharded (global) one
+        # so a connection's bytes do not depend on which rank owns it
+        first_off = self.pt_off[self.chain_first] if self.n_chains else np.zeros(0, dtype=np.uint64)
+        self.chain_stream_start = (first_off.astype(np.uint64) if chain_stream_start is None
+                                   else np.asarray(chain_stream_start, dtype=np.uint64))
+        self._contiguous_fill = chain_stream_start is None
+
+    def fill_plan(self):
+        """[(arena_offset, nbytes, stream_start)] covering every chain's plaintext."""
+        if self._contiguous_fill:
+            return [(0, self.pt_bytes, 0)]
+        plan = []
+        for c in range(self.n_chains):
+            a = int(self.chain_first[c])
+            b = a + int(self.chain_count[c]) - 1
+            off = int(self.pt_off[a])
+            end = int(self.pt_off[b]) + int(self.pt_len[b])
+            plan.append((off, end - off, int(self.chain_stream_start[c])))
+        return plan
+
+    def host_plaintext(self, fill_fn):
+        """Host copy of the plaintext arena; fill_fn(n, seed, start) -> uint8 array."""
+        out = np.zeros(self.pt_bytes, dtype=np.uint8)
+        for off, n, start in self.fill_plan():
+            out[off:off + n] = fill_fn(n, self.seed, start)
+        return out
 
     def _rec_groups(self):
         for gi, g in enumerate(self.groups):
@@ -155,7 +182,8 @@ class Workload:
             d.upload(np.frombuffer(ch, dtype=np.uint8))
             self.launches.append((var, d, len(idx)))
         if fill:
-            fill_pattern(self.d_pt, self.pt_bytes, self.seed, 0, 0, stream)
+            for off, n, start in self.fill_plan():
+                fill_pattern(self.d_pt, n, self.seed, start, off, stream)
         self.d_wire.zero(stream)
         return self
 
@@ -211,8 +239,10 @@ def cfg4(nconn=4096, recs_per_conn=256, pt_len=16384, seed=4, rank=0, world=1):
     mine = np.arange(rank, nconn, world)
     g = Group("AES128-SHA", (3, 3), [keys[i] for i in mine], ivs[mine], [mks[i] for i in mine],
               [fivs[i] for i in mine], np.zeros(len(mine), dtype=np.uint64), recs_per_conn, pt_len)
+    per_conn = recs_per_conn * _round_up(pt_len, 16)
     return Workload("cfg4: %d conns x %d records of %d B, AES128-SHA, chained (rank %d/%d)"
-                    % (nconn, recs_per_conn, pt_len, rank, world), [g], seed + 1000 * rank)
+                    % (nconn, recs_per_conn, pt_len, rank, world), [g], seed,
+                    chain_stream_start=mine.astype(np.uint64) * per_conn)
 
 
 def cfg5(n=65536, pt_len=16384, seed=5):
