@@ -37,7 +37,8 @@ def parse():
     ap.add_argument("--records", type=int, default=None, help="override record count (debug)")
     ap.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline")
     ap.add_argument("--no-check", action="store_true", help="skip the full-batch parity check")
-    ap.add_argument("--host-inclusive", action="store_true", default=True)
+    ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false",
+                    help="skip the PCIe-inclusive measurement (profiling runs)")
     ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
     return ap.parse_args()
 

@@ -21,9 +21,20 @@ class ShardGroup:
         self.local = int(os.environ.get("LOCAL_RANK", str(self.rank)))
         self.dist = None
         if self.world > 1:
+            import sys
             import torch.distributed as dist
             if not dist.is_initialized():
-                dist.init_process_group(backend)
+                # gloo prints connection banners on fd 1; keep stdout for the
+                # bench's single JSON line
+                sys.stdout.flush()
+                saved = os.dup(1)
+                os.dup2(2, 1)
+                try:
+                    dist.init_process_group(backend)
+                finally:
+                    sys.stdout.flush()
+                    os.dup2(saved, 1)
+                    os.close(saved)
             self.dist = dist
 
     def barrier(self):
