@@ -182,10 +182,31 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state *st, uint32_t pt_len, uint32_t 
 /* ---- batch seal / open (device pointers, async on stream) ---------------
  * wire_len[r] receives the bytes written for record r (header included), 0
  * for an empty record, or a negative TLSGPU_E* code.  All chains of one
- * launch must use connection states of `variant`. */
+ * launch must use connection states of `variant`; `records` has `nrecords`
+ * entries (chains index into it). */
+/* Device workspace for a seal of `nrecords` descriptors (AES suites: per
+ * record 32 B of metadata + a 64 B CBC-tail slot).  Pass it to
+ * tlsgpu_seal_dev, or pass NULL there to use a library-owned per-device
+ * workspace (then calls on different streams must not overlap). */
+size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords);
 int tlsgpu_seal_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_record *records,
-                    const uint8_t *pt, uint8_t *wire, tlsgpu_conn_state *states, int32_t *wire_len,
-                    uint32_t variant, tlsgpu_stream s);
+                    uint32_t nrecords, const uint8_t *pt, uint8_t *wire, tlsgpu_conn_state *states,
+                    int32_t *wire_len, uint32_t variant, void *workspace, size_t workspace_bytes,
+                    tlsgpu_stream s);
+/* ---- seal pipeline: successive tlsgpu_pipeline_seal calls overlap the MAC
+ * phase of call k+1 with the cipher phase of call k (AES suites; two
+ * library-owned streams, double-buffered workspace).  Inputs must be ready
+ * when a call is made and stay valid, and outputs are complete, only after
+ * tlsgpu_pipeline_synchronize.  Optional events bracket the cipher kernel. */
+typedef struct tlsgpu_pipeline_s *tlsgpu_pipeline;
+int tlsgpu_pipeline_create(tlsgpu_pipeline *p, uint32_t max_records);
+int tlsgpu_pipeline_destroy(tlsgpu_pipeline p);
+int tlsgpu_pipeline_synchronize(tlsgpu_pipeline p);
+int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain *chains, uint32_t nchains,
+                         const tlsgpu_record *records, uint32_t nrecords, const uint8_t *pt, uint8_t *wire,
+                         tlsgpu_conn_state *states, int32_t *wire_len, uint32_t variant,
+                         tlsgpu_event cipher_start, tlsgpu_event cipher_stop);
+
 /* status[r] = plaintext length, or TLSGPU_ALERT_* */
 int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_open_record *records,
                     const uint8_t *wire, uint8_t *pt, tlsgpu_conn_state *states, int32_t *status,

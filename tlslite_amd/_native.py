@@ -79,7 +79,12 @@ SIGNATURES = [
     ("tlsgpu_conn_state_get_rc4", _i, [_vp, _u8p, ctypes.POINTER(_u32), ctypes.POINTER(_u32)]),
     ("tlsgpu_conn_state_variant", _i, [_vp, ctypes.POINTER(_u32)]),
     ("tlsgpu_seal_wire_len", _i, [_vp, _u32, ctypes.POINTER(_u32)]),
-    ("tlsgpu_seal_dev", _i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("tlsgpu_seal_workspace_bytes", _sz, [_u32]),
+    ("tlsgpu_seal_dev", _i, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
+    ("tlsgpu_pipeline_create", _i, [ctypes.POINTER(_vp), _u32]),
+    ("tlsgpu_pipeline_destroy", _i, [_vp]),
+    ("tlsgpu_pipeline_synchronize", _i, [_vp]),
+    ("tlsgpu_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp]),
     ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
     ("tlsgpu_cipher_dev", _i, [_vp, _u32, _vp, _vp, _vp, _i, _i, _vp]),
     ("tlsgpu_fill_pattern", _i, [_vp, _sz, _u64, _u64, _vp]),

@@ -72,6 +72,14 @@ struct QuadAes {
         y ^= quad_dpp<0x93>(look<1, 3>(x) & 0xff000000u);
         return y;
     }
+    // one block of one chain
+    template <int NR>
+    __device__ __forceinline__ uint32_t encrypt1(uint32_t a, const uint32_t* ka) const {
+        a ^= ka[0];
+#pragma unroll
+        for (int r = 1; r < NR; r++) a = round<0>(a, ka[r]);
+        return last(a, ka[NR]);
+    }
     // two independent blocks (chains a and b) interleaved round by round
     template <int NR>
     __device__ __forceinline__ void encrypt2(uint32_t& a, uint32_t& b, const uint32_t* ka, const uint32_t* kb) const {

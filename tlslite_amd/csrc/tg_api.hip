@@ -399,14 +399,122 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state* st, uint32_t pt_len, uint32_t*
     return 0;
 }
 
-int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* records, const uint8_t* pt,
-                    uint8_t* wire, tlsgpu_conn_state* states, int32_t* wire_len, uint32_t variant, tlsgpu_stream s) {
+size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords) { return seal_workspace_bytes(nrecords); }
+
+int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* records, uint32_t nrecords,
+                    const uint8_t* pt, uint8_t* wire, tlsgpu_conn_state* states, int32_t* wire_len, uint32_t variant,
+                    void* workspace, size_t workspace_bytes, tlsgpu_stream s) {
     if (nchains == 0) return 0;
     if (!chains || !records || !pt || !wire || !states || !wire_len) return fail(TLSGPU_EINVAL, "null pointer");
+    uint8_t* ws = static_cast<uint8_t*>(workspace);
+    if (seal_needs_workspace(variant)) {
+        const size_t need = seal_workspace_bytes(nrecords);
+        if (ws && workspace_bytes < need) return fail(TLSGPU_EINVAL, "workspace too small");
+        if (!ws) {  // library-owned, per device, grow-only (not for concurrent calls on several streams)
+            static thread_local void* own[64] = {nullptr};
+            static thread_local size_t own_bytes[64] = {0};
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            dev &= 63;
+            if (own_bytes[dev] < need) {
+                if (own[dev]) TG_HIP(hipFree(own[dev]));
+                own[dev] = nullptr;
+                own_bytes[dev] = 0;
+                TG_HIP(hipMalloc(&own[dev], need));
+                own_bytes[dev] = need;
+            }
+            ws = static_cast<uint8_t*>(own[dev]);
+        }
+    }
+    static uint32_t epoch_ctr = 0;
+    const uint32_t epoch = __atomic_add_fetch(&epoch_ctr, 1, __ATOMIC_RELAXED);
     bool known = false;
-    hipError_t e = launch_seal(variant, chains, nchains, records, pt, wire, S(states), wire_len, HS(s), &known);
+    hipError_t e = launch_seal(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len, ws, epoch,
+                               HS(s), &known);
     if (!known) return fail(TLSGPU_EINVAL, "unsupported seal variant");
     if (e != hipSuccess) return fail_hip(e, "seal launch");
+    return 0;
+}
+
+// ---------------------------------------------------------------- pipeline
+struct tlsgpu_pipeline_s {
+    int dev;
+    hipStream_t mac_s, cbc_s;
+    hipEvent_t mac_done[2], cbc_done[2];
+    void* ws[2];
+    size_t ws_bytes;
+    uint64_t k;
+};
+
+int tlsgpu_pipeline_create(tlsgpu_pipeline* out, uint32_t max_records) {
+    if (!out) return fail(TLSGPU_EINVAL, "null");
+    tlsgpu_pipeline p = new tlsgpu_pipeline_s();
+    TG_HIP(hipGetDevice(&p->dev));
+    TG_HIP(hipStreamCreateWithFlags(&p->mac_s, hipStreamNonBlocking));
+    TG_HIP(hipStreamCreateWithFlags(&p->cbc_s, hipStreamNonBlocking));
+    for (int i = 0; i < 2; i++) {
+        TG_HIP(hipEventCreateWithFlags(&p->mac_done[i], hipEventDisableTiming));
+        TG_HIP(hipEventCreateWithFlags(&p->cbc_done[i], hipEventDisableTiming));
+    }
+    p->ws_bytes = seal_workspace_bytes(max_records ? max_records : 1);
+    for (int i = 0; i < 2; i++) TG_HIP(hipMalloc(&p->ws[i], p->ws_bytes));
+    p->k = 0;
+    *out = p;
+    return 0;
+}
+
+int tlsgpu_pipeline_destroy(tlsgpu_pipeline p) {
+    if (!p) return 0;
+    (void)hipStreamSynchronize(p->mac_s);
+    (void)hipStreamSynchronize(p->cbc_s);
+    for (int i = 0; i < 2; i++) {
+        (void)hipFree(p->ws[i]);
+        (void)hipEventDestroy(p->mac_done[i]);
+        (void)hipEventDestroy(p->cbc_done[i]);
+    }
+    (void)hipStreamDestroy(p->mac_s);
+    (void)hipStreamDestroy(p->cbc_s);
+    delete p;
+    return 0;
+}
+
+int tlsgpu_pipeline_synchronize(tlsgpu_pipeline p) {
+    TG_HIP(hipStreamSynchronize(p->mac_s));
+    TG_HIP(hipStreamSynchronize(p->cbc_s));
+    return 0;
+}
+
+int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain* chains, uint32_t nchains,
+                         const tlsgpu_record* records, uint32_t nrecords, const uint8_t* pt, uint8_t* wire,
+                         tlsgpu_conn_state* states, int32_t* wire_len, uint32_t variant, tlsgpu_event cipher_start,
+                         tlsgpu_event cipher_stop) {
+    if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
+    if (nchains == 0) return 0;
+    if (!chains || !records || !pt || !wire || !states || !wire_len) return fail(TLSGPU_EINVAL, "null pointer");
+    if (seal_workspace_bytes(nrecords) > p->ws_bytes) return fail(TLSGPU_EINVAL, "nrecords > pipeline max_records");
+    static uint32_t epoch_ctr = 0x80000000u;
+    const uint32_t epoch = __atomic_add_fetch(&epoch_ctr, 1, __ATOMIC_RELAXED);
+    const int i = (int)(p->k & 1);
+    // workspace i was last read by the cipher phase of call k-2
+    if (p->k >= 2) TG_HIP(hipStreamWaitEvent(p->mac_s, p->cbc_done[i], 0));
+    bool known = false;
+    hipError_t e = hipSuccess;
+    if (seal_needs_workspace(variant)) {
+        e = launch_seal_phases(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len,
+                               static_cast<uint8_t*>(p->ws[i]), epoch, p->mac_s, p->mac_done[i], p->cbc_s,
+                               reinterpret_cast<hipEvent_t>(cipher_start), reinterpret_cast<hipEvent_t>(cipher_stop),
+                               &known);
+    } else {
+        // single-kernel variants run on the cipher stream, in order with earlier calls
+        if (cipher_start) TG_HIP(hipEventRecord(reinterpret_cast<hipEvent_t>(cipher_start), p->cbc_s));
+        e = launch_seal(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len, nullptr, epoch,
+                        p->cbc_s, &known);
+        if (e == hipSuccess && cipher_stop) e = hipEventRecord(reinterpret_cast<hipEvent_t>(cipher_stop), p->cbc_s);
+    }
+    if (!known) return fail(TLSGPU_EINVAL, "unsupported seal variant");
+    if (e != hipSuccess) return fail_hip(e, "pipeline seal");
+    TG_HIP(hipEventRecord(p->cbc_done[i], p->cbc_s));
+    p->k++;
     return 0;
 }
 

@@ -7,6 +7,7 @@
 #include <stdlib.h>
 #include "tg_device.h"
 #include "tg_aesq.h"
+#include "tg_aes3.h"
 #include "tg_launch.h"
 
 namespace tg {
@@ -460,6 +461,116 @@ static hipError_t set_lds(K kern, uint32_t bytes) {
                                (int)bytes);
 }
 
+// AES implementation: 0 = split (prefix/mac/cbc, default), 1 = fused quad
+// kernel (TLSGPU_SEAL_IMPL=fused), 2 = one lane per chain (=lane).  A/B only.
+static int aes_impl() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("TLSGPU_SEAL_IMPL");
+        v = (e && e[0] == 'f') ? 1 : (e && e[0] == 'l') ? 2 : 0;
+    }
+    return v;
+}
+static uint32_t debug_skip_flags() {
+    static uint32_t skip = 0xffffffffu;
+    if (skip == 0xffffffffu) {  // TLSGPU_DEBUG_SKIP: 1 = no CBC bulk, 2 = no MAC bulk (timing ablation only)
+        const char* e = getenv("TLSGPU_DEBUG_SKIP");
+        skip = e ? (uint32_t)atoi(e) : 0u;
+    }
+    return skip;
+}
+static int cu_count() {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (ncu <= 0) ncu = 256;
+    }
+    return ncu;
+}
+
+size_t seal_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * (sizeof(RecMeta) + TAIL_SLOT); }
+
+// phase 1 (stream s1): meta memset + seqnum prefix + per-record MAC / tail / header
+template <int NR, int MAC, bool SSL3>
+static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                                   uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
+                                   int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s) {
+    constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : TLSGPU_CIPHER_AES256;
+    RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
+    uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
+    hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(RecMeta), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((prefix_kernel<CID, MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains,
+                       recs, states, wire_len, meta, nrecords, epoch);
+    hipLaunchKernelGGL((mac_kernel<MAC, SSL3>), dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords, pt, wire,
+                       states, wire_len, meta, tails, epoch, debug_skip_flags());
+    return hipGetLastError();
+}
+
+// phase 2 (stream s2, after phase 1): CBC over [explicit IV | P blocks | tail]
+template <int NR>
+static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                                   uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
+                                   uint8_t* ws, uint32_t epoch, hipStream_t s) {
+    RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
+    uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
+    auto kern = cbc_kernel<NR>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = set_lds(kern, AES_LDS_BYTES);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    uint32_t cpw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
+    cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
+    hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C3_THREADS), AES_LDS_BYTES, s, chains, nchains, recs,
+                       nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
+    return hipGetLastError();
+}
+
+template <int NR, int MAC, bool SSL3>
+static hipError_t launch_seal_split(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
+                                    int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s) {
+    hipError_t e = launch_mac_phase<NR, MAC, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,
+                                                   epoch, s);
+    if (e != hipSuccess) return e;
+    return launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s);
+}
+
+// Split AES seal with the two phases on two streams (pipeline API).
+hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
+                              const tlsgpu_record* recs, uint32_t nrecords, const uint8_t* pt, uint8_t* wire,
+                              ConnState* states, int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s1,
+                              hipEvent_t mac_done, hipStream_t s2, hipEvent_t cbc_start, hipEvent_t cbc_stop,
+                              bool* known) {
+    *known = true;
+    hipError_t e = hipSuccess;
+#define TG_PH(CID, NR, MAC_ID, SSL3)                                                                            \
+    if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3)) {                                                          \
+        e = launch_mac_phase<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,   \
+                                               epoch, s1);                                                       \
+        if (e != hipSuccess) return e;                                                                           \
+        if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                          \
+        if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                                   \
+        if (cbc_start && (e = hipEventRecord(cbc_start, s2)) != hipSuccess) return e;                           \
+        e = launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s2);              \
+        if (e == hipSuccess && cbc_stop) e = hipEventRecord(cbc_stop, s2);                                       \
+        return e;                                                                                                \
+    }
+    TG_PH(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)
+    TG_PH(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, false)
+    TG_PH(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA256, false)
+    TG_PH(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false)
+    TG_PH(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)
+    TG_PH(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)
+#undef TG_PH
+    *known = false;
+    return hipSuccess;
+}
+
 template <int NR, int MAC, bool SSL3>
 static hipError_t launch_seal_aesq(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
@@ -471,44 +582,27 @@ static hipError_t launch_seal_aesq(const tlsgpu_chain* chains, uint32_t nchains,
         if (e != hipSuccess) return e;
         attr = true;
     }
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (ncu <= 0) ncu = 256;
-    }
-    uint32_t cpw = (nchains + ncu - 1) / (uint32_t)ncu;
+    const uint32_t ncu = (uint32_t)cu_count();
+    uint32_t cpw = (nchains + ncu - 1) / ncu;
     cpw = cpw < 1 ? 1 : (cpw > (uint32_t)Q_CHAINS ? (uint32_t)Q_CHAINS : cpw);
     dim3 grid((nchains + cpw - 1) / cpw);
-    static uint32_t skip = 0xffffffffu;
-    if (skip == 0xffffffffu) {  // TLSGPU_DEBUG_SKIP: 1 = no CBC bulk, 2 = no MAC bulk (timing ablation only)
-        const char* e = getenv("TLSGPU_DEBUG_SKIP");
-        skip = e ? (uint32_t)atoi(e) : 0u;
-    }
+    const uint32_t skip = debug_skip_flags();
     hipLaunchKernelGGL(kern, grid, dim3(Q_THREADS), Q_LDS_BYTES, s, chains, nchains, recs, pt, wire, states, wire_len,
                        cpw, skip);
     return hipGetLastError();
 }
 
-// TLSGPU_SEAL_IMPL=lane selects the one-lane-per-chain AES kernel (A/B only)
-static bool use_quad_aes() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TLSGPU_SEAL_IMPL");
-        v = (e && e[0] == 'l') ? 0 : 1;
-    }
-    return v == 1;
-}
-
 template <class C, int MAC, bool SSL3>
 static hipError_t launch_seal_t(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
-                                const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
-                                hipStream_t s) {
+                                uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
+                                int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s) {
     if constexpr (CipherTraits<C>::ID == TLSGPU_CIPHER_AES128 || CipherTraits<C>::ID == TLSGPU_CIPHER_AES256) {
-        if (use_quad_aes())
-            return launch_seal_aesq<CipherTraits<C>::ID == TLSGPU_CIPHER_AES128 ? 10 : 14, MAC, SSL3>(
-                chains, nchains, recs, pt, wire, states, wire_len, s);
+        constexpr int NR = CipherTraits<C>::ID == TLSGPU_CIPHER_AES128 ? 10 : 14;
+        if (aes_impl() == 0)
+            return launch_seal_split<NR, MAC, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,
+                                                    epoch, s);
+        if (aes_impl() == 1)
+            return launch_seal_aesq<NR, MAC, SSL3>(chains, nchains, recs, pt, wire, states, wire_len, s);
     }
     auto kern = seal_kernel<C, MAC, SSL3>;
     constexpr uint32_t lds = CipherTraits<C>::LDS;
@@ -523,13 +617,19 @@ static hipError_t launch_seal_t(const tlsgpu_chain* chains, uint32_t nchains, co
     return hipGetLastError();
 }
 
+bool seal_needs_workspace(uint32_t variant) {
+    const uint32_t c = variant & 0xff;
+    return aes_impl() == 0 && (c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256);
+}
+
 hipError_t launch_seal(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
-                       const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len, hipStream_t s,
-                       bool* known) {
+                       uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
+                       uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known) {
     *known = true;
 #define TG_SEAL_CASE(CIPHER_ID, CTYPE, MAC_ID, SSL3)                                                      \
     if (variant == TLSGPU_VARIANT(CIPHER_ID, MAC_ID, SSL3))                                               \
-        return launch_seal_t<CTYPE, MAC_ID, SSL3>(chains, nchains, recs, pt, wire, states, wire_len, s);
+        return launch_seal_t<CTYPE, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws, \
+                                                  epoch, s);
     // TLS 1.0-1.2 HMAC suites (constants.py:159-201)
     TG_SEAL_CASE(TLSGPU_CIPHER_AES128, AesCbc<10>, TLSGPU_MAC_SHA1, false)
     TG_SEAL_CASE(TLSGPU_CIPHER_AES256, AesCbc<14>, TLSGPU_MAC_SHA1, false)

@@ -110,12 +110,54 @@ def make_chains(state_idx, first, count):
     return ch
 
 
-def seal_dev(chains, nchains, records, pt, wire, states, wire_len, variant, stream=None):
-    """Device-resident batch seal (all pointers are DeviceBuffer / addresses)."""
+def seal_workspace_bytes(nrecords):
+    return int(N.lib.tlsgpu_seal_workspace_bytes(int(nrecords)))
+
+
+def seal_dev(chains, nchains, records, nrecords, pt, wire, states, wire_len, variant, workspace=None, stream=None):
+    """Device-resident batch seal (all pointers are DeviceBuffer / addresses).
+    workspace: DeviceBuffer of >= seal_workspace_bytes(nrecords), or None for
+    the library-owned one (then no concurrent calls on other streams)."""
     def p(x):
         return x.ptr if isinstance(x, DeviceBuffer) else ctypes.c_void_p(x)
-    N.call("tlsgpu_seal_dev", p(chains), nchains, p(records), p(pt), p(wire), p(states), p(wire_len), variant,
+    N.call("tlsgpu_seal_dev", p(chains), nchains, p(records), int(nrecords), p(pt), p(wire), p(states), p(wire_len),
+           variant, None if workspace is None else p(workspace), 0 if workspace is None else workspace.nbytes,
            stream.handle if stream is not None else None)
+
+
+class SealPipeline:
+    """Overlapped batch seal (tlsgpu_pipeline_*): the per-record MAC phase of
+    call k+1 runs while the CBC phase of call k is still encrypting, on two
+    library-owned streams with double-buffered workspaces.  Each call has the
+    semantics of seal_dev; results are complete after synchronize()."""
+
+    def __init__(self, max_records):
+        h = ctypes.c_void_p()
+        N.call("tlsgpu_pipeline_create", ctypes.byref(h), int(max_records))
+        self.handle = h
+        self.max_records = int(max_records)
+
+    def seal(self, chains, nchains, records, nrecords, pt, wire, states, wire_len, variant,
+             cipher_start=None, cipher_stop=None):
+        def p(x):
+            return x.ptr if isinstance(x, DeviceBuffer) else ctypes.c_void_p(x)
+        N.call("tlsgpu_pipeline_seal", self.handle, p(chains), nchains, p(records), int(nrecords), p(pt), p(wire),
+               p(states), p(wire_len), variant, cipher_start.handle if cipher_start is not None else None,
+               cipher_stop.handle if cipher_stop is not None else None)
+
+    def synchronize(self):
+        N.call("tlsgpu_pipeline_synchronize", self.handle)
+
+    def close(self):
+        if self.handle is not None and self.handle.value:
+            N.call("tlsgpu_pipeline_destroy", self.handle)
+        self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def seal(states, records, stream=None):
@@ -189,7 +231,7 @@ def seal(states, records, stream=None):
         d_ch = DeviceBuffer(ctypes.sizeof(c))
         d_ch.upload(np.frombuffer(c, dtype=np.uint8), stream=stream)
         chain_bufs.append(d_ch)
-        seal_dev(d_ch, len(chs), d_recs, d_pt, d_wire, d_states, d_len, var, stream)
+        seal_dev(d_ch, len(chs), d_recs, nrec, d_pt, d_wire, d_states, d_len, var, None, stream)
     if stream is not None:
         stream.synchronize()
     wire_host = d_wire.download()

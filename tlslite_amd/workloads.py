@@ -191,19 +191,42 @@ class Workload:
         N.call("tlsgpu_memcpy_d2d", self.d_states.ptr, self.d_states0.ptr, self.d_states.nbytes,
                stream.handle if stream else None)
 
-    def launch(self, streams=None):
-        """Seal every record once (one kernel launch per suite variant; with
-        several streams the variants run concurrently)."""
+    def launch(self, streams=None, pipeline=None, cipher_events=None):
+        """Seal every record once (one seal call per suite variant; with
+        several streams the variants run concurrently).  With a SealPipeline
+        the calls are queued on it instead (MAC/cipher phases overlap across
+        calls); cipher_events=(start, stop) bracket the first call's cipher
+        kernel."""
+        if pipeline is not None:
+            for i, (var, d_ch, nch) in enumerate(self.launches):
+                ev = cipher_events if (cipher_events and i == 0) else (None, None)
+                pipeline.seal(d_ch, nch, self.d_recs, self.n_records, self.d_pt, self.d_wire, self.d_states,
+                              self.d_len, var, ev[0], ev[1])
+            return
+        if not hasattr(self, "d_ws"):
+            nb = int(N.lib.tlsgpu_seal_workspace_bytes(self.n_records))
+            self.d_ws = [DeviceBuffer(nb) for _ in self.launches]  # one per launch: variants may run concurrently
         for i, (var, d_ch, nch) in enumerate(self.launches):
             s = None if not streams else streams[i % len(streams)]
-            N.call("tlsgpu_seal_dev", d_ch.ptr, nch, self.d_recs.ptr, self.d_pt.ptr, self.d_wire.ptr,
-                   self.d_states.ptr, self.d_len.ptr, var, s.handle if s else None)
+            ws = self.d_ws[i]
+            N.call("tlsgpu_seal_dev", d_ch.ptr, nch, self.d_recs.ptr, self.n_records, self.d_pt.ptr, self.d_wire.ptr,
+                   self.d_states.ptr, self.d_len.ptr, var, ws.ptr, ws.nbytes, s.handle if s else None)
+
+    def dominant_kernel(self):
+        """Name (rocprof stem) of the kernel that dominates the first launch."""
+        var = self.launches[0][0]
+        c, m = var & 0xff, (var >> 8) & 0xff
+        if c in (N.CIPHER_AES128, N.CIPHER_AES256) and m in (N.MAC_SHA1, N.MAC_SHA256):
+            return "cbc_kernel<%d>" % (10 if c == N.CIPHER_AES128 else 14)
+        return "seal_kernel"
 
     def free(self):
         for name in ("d_pt", "d_wire", "d_len", "d_recs", "d_states", "d_states0"):
             b = getattr(self, name, None)
             if b is not None:
                 b.free()
+        for b in getattr(self, "d_ws", []):
+            b.free()
         for _, d, _ in getattr(self, "launches", []):
             d.free()
 
