@@ -182,8 +182,7 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
     const uint32_t fiv = st->fixed_iv[q];
     const uint32_t E = st->explicit_iv ? 16u : 0u;
     bool any = false;
-#pragma unroll
-    for (int r = 0; r <= NR; r++) k[r] = st->ek[4 * r + q];
+    QuadAes::round_keys<NR>(st->ek, q, k);
     for (uint32_t j = 0; j < ch.count; j++) {
         const uint32_t r = ch.first + j;
         if (r >= nrecords) break;
@@ -201,6 +200,7 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
         }
         uint8_t* O = B + E + 4 * q;
         const uint32_t nb = (debug_skip & 1) ? 0u : (n >> 4);
+        // whitening: block ^ previous ciphertext ^ k[0] as one 3-input v_bitop3
         uint32_t f[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) f[i] = (uint32_t)i < nb ? ld32(P + 16 * i, al) : 0u;
@@ -216,7 +216,7 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
 #pragma unroll
             for (int i = 0; i < 8; i++) {
                 if (b0 + i < nb) {
-                    iv = aes.encrypt1<NR>(c[i] ^ iv, k);
+                    iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(c[i], iv, k[0], 0x96), k);
                     st32(O + 16 * (b0 + i), iv, al);
                 }
             }

@@ -56,26 +56,50 @@ struct QuadAes {
         constexpr uint32_t sel = 0x0c000000u | (2u << 16) | ((4u + B) << 8) | 0u;
         return lds_read32(perm(s, T >= 2 ? hi : lo, sel) + (T & 1) * 128);
     }
+    // Column q of the next state = T0[b0(q)] ^ T1[b1(q+1)] ^ T2[b2(q+2)] ^ T3[b3(q+3)] ^ k[q], with
+    // the lookup of byte b done by lane q+b.  XOR tree: dpp2(t2) ^ dpp3(t3) = dpp2(t2 ^ dpp1(t3)),
+    // and the round key rides in that inner term: k2 is the key column of lane q+2 (round_keys()),
+    // so once the T0/T1 lookups return only two dependent DPP XORs remain (a chain needs four).
+    // The T2/T3 lookups are issued first: they feed the inner term.
     template <int R>
-    __device__ __forceinline__ uint32_t round(uint32_t x, uint32_t k) const {
-        uint32_t y = look<0, 0>(x) ^ k;
-        y ^= quad_dpp<0x39>(look<1, 1>(x));  // T1 term of column q comes from lane q+1
-        y ^= quad_dpp<0x4E>(look<2, 2>(x));  // T2 term from lane q+2
-        y ^= quad_dpp<0x93>(look<3, 3>(x));  // T3 term from lane q+3
-        return y;
+    __device__ __forceinline__ uint32_t round(uint32_t x, uint32_t k2) const {
+        const uint32_t t2 = look<2, 2>(x);
+        const uint32_t t3 = look<3, 3>(x);
+        const uint32_t t0 = look<0, 0>(x);
+        const uint32_t t1 = look<1, 1>(x);
+        const uint32_t u = (t2 ^ k2) ^ quad_dpp<0x39>(t3);
+        const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
+        return z ^ quad_dpp<0x4E>(u);
+    }
+    // per-lane round keys in the layout round()/last() expect: k[0] = whitening column q,
+    // k[r >= 1] = column (q+2)&3 of round key r
+    template <int NR>
+    static __device__ __forceinline__ void round_keys(const uint32_t* ek, uint32_t q, uint32_t* k) {
+        k[0] = ek[q];
+#pragma unroll
+        for (int r = 1; r <= NR; r++) k[r] = ek[4 * r + ((q + 2) & 3)];
     }
     __device__ __forceinline__ uint32_t last(uint32_t x, uint32_t k) const {
         // S-box byte r sits at byte r of table (r+2)&3
-        uint32_t y = (look<2, 0>(x) & 0xffu) ^ k;
-        y ^= quad_dpp<0x39>(look<3, 1>(x) & 0xff00u);
-        y ^= quad_dpp<0x4E>(look<0, 2>(x) & 0xff0000u);
-        y ^= quad_dpp<0x93>(look<1, 3>(x) & 0xff000000u);
-        return y;
+        const uint32_t s2 = look<0, 2>(x) & 0xff0000u;
+        const uint32_t s3 = look<1, 3>(x) & 0xff000000u;
+        const uint32_t s0 = look<2, 0>(x) & 0xffu;
+        const uint32_t s1 = look<3, 1>(x) & 0xff00u;
+        const uint32_t u = (s2 ^ k) ^ quad_dpp<0x39>(s3);
+        const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
+        return z ^ quad_dpp<0x4E>(u);
     }
     // one block of one chain
     template <int NR>
     __device__ __forceinline__ uint32_t encrypt1(uint32_t a, const uint32_t* ka) const {
         a ^= ka[0];
+#pragma unroll
+        for (int r = 1; r < NR; r++) a = round<0>(a, ka[r]);
+        return last(a, ka[NR]);
+    }
+    // one block whose input is already whitened (x = block ^ k[0])
+    template <int NR>
+    __device__ __forceinline__ uint32_t encrypt_w(uint32_t a, const uint32_t* ka) const {
 #pragma unroll
         for (int r = 1; r < NR; r++) a = round<0>(a, ka[r]);
         return last(a, ka[NR]);
@@ -241,8 +265,8 @@ seal_aesq_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, cons
     uint32_t ivA = 0, ivB = 0;
 #pragma unroll
     for (int r = 0; r <= NR; r++) {
-        kA[r] = okA ? sA->ek[4 * r + q] : 0u;
-        kB[r] = okB ? sB->ek[4 * r + q] : 0u;
+        kA[r] = okA ? sA->ek[r == 0 ? q : 4 * r + ((q + 2) & 3)] : 0u;
+        kB[r] = okB ? sB->ek[r == 0 ? q : 4 * r + ((q + 2) & 3)] : 0u;
     }
     if (okA) ivA = sA->iv[q];
     if (okB) ivB = sB->iv[q];
