@@ -21,6 +21,21 @@
 
 namespace tg {
 
+// wave priority from a runtime value (s_setprio takes an immediate)
+__device__ __forceinline__ void set_prio(uint32_t p) {
+    switch (p) {
+        case 0: __builtin_amdgcn_s_setprio(0); break;
+        case 1: __builtin_amdgcn_s_setprio(1); break;
+        case 2: __builtin_amdgcn_s_setprio(2); break;
+        default: __builtin_amdgcn_s_setprio(3); break;
+    }
+}
+// debug_skip bits 4-5 / 6-7: (priority + 1) of the CBC / MAC waves, 0 = built-in default
+__device__ __forceinline__ uint32_t prio_of(uint32_t debug_skip, int shift, uint32_t dflt) {
+    const uint32_t v = (debug_skip >> shift) & 3u;
+    return v ? v - 1 : dflt;
+}
+
 struct RecMeta {
     uint64_t seq;
     uint32_t state;
@@ -92,6 +107,7 @@ __global__ void __launch_bounds__(256) mac_kernel(const tlsgpu_record* __restric
     if (r >= nrecords) return;
     const RecMeta mt = meta[r];
     if (mt.epoch != epoch || mt.status != 1) return;
+    set_prio(prio_of(debug_skip, 6, 0));
     const ConnState* st = states + mt.state;
     const tlsgpu_record R = recs[r];
     const uint32_t n = R.pt_len;
@@ -174,7 +190,7 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
     const tlsgpu_chain ch = chains[cid];
     ConnState* st = states + ch.state;
     // the prefix kernel validated the state: any record it marked status 1 belongs to a matching state
-    __builtin_amdgcn_s_setprio(1);
+    set_prio(prio_of(debug_skip, 4, 1));
     QuadAes aes;
     aes.init();
     uint32_t k[NR + 1];

@@ -473,7 +473,7 @@ static int aes_impl() {
 }
 static uint32_t debug_skip_flags() {
     static uint32_t skip = 0xffffffffu;
-    if (skip == 0xffffffffu) {  // TLSGPU_DEBUG_SKIP: 1 = no CBC bulk, 2 = no MAC bulk (timing ablation only)
+    if (skip == 0xffffffffu) {  // TLSGPU_DEBUG_SKIP: 1 = no CBC bulk, 2 = no MAC bulk, bits 4-7 wave priorities (tg_aes3.h); timing experiments only
         const char* e = getenv("TLSGPU_DEBUG_SKIP");
         skip = e ? (uint32_t)atoi(e) : 0u;
     }

@@ -7,7 +7,8 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 CFG=${1:-cfg2}
-OUT=${2:-$R/gpurun_out/pmck_$CFG}
+OUT=${2:-gpurun_out/pmck_$CFG}
+case $OUT in /*) ;; *) OUT=$R/$OUT ;; esac
 shift 2 || true
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
