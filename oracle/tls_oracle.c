@@ -533,7 +533,10 @@ long ora_open(ora_conn *c, int ctype, uint8_t *b, size_t n, size_t *pt_off) {
     if (c->bs) {
         if (n % (size_t)c->bs) return ORA_ALERT_DECRYPTION_FAILED;          /* :964-968 */
         cbc_decrypt(c, b, n);
-        if (c->vmaj == 3 && c->vmin >= 2) { start = (size_t)c->bs; len -= (size_t)c->bs; }  /* :970-971 */
+        if (c->vmaj == 3 && c->vmin >= 2) {                                 /* :970-971 (b[bs:] of a shorter b is empty) */
+            start = (size_t)c->bs;
+            len = n > (size_t)c->bs ? n - (size_t)c->bs : 0;
+        }
         if (len == 0) return ORA_ALERT_DECRYPTION_FAILED;                  /* :973-977 */
         uint8_t pl = b[start + len - 1];
         if ((size_t)pl + 1 > len) { padGood = 0; totalPad = 0; }

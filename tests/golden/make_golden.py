@@ -132,6 +132,9 @@ class FakeSock:
         self.out = bytearray()
         self.writes = []
 
+    def close(self):
+        pass
+
     def send(self, s):
         self.out += s
         self.writes.append(bytes(s))
@@ -296,9 +299,62 @@ def main():
                               **keys, **de,
                               "writes": [wire_entry(w) for w in writes],
                               "final": final_state(r, suite)})
-    # (v) open-side vectors: decrypt+verify via _decryptRecord (:958-1044) of the
-    #     sealed records in (iii) are covered by round trips; here record the alert
-    #     the reference raises for tampered records.
+    # (v) open: _decryptRecord (:958-1044) on one read state over a chain of valid,
+    #     tampered and malformed bodies (empty, IV-only, not a block multiple, garbage).
+    #     _sendError (:524-529) shuts the layer down after an alert; the batch API keeps
+    #     going, so each body is opened on the SAME state object again (the alert only
+    #     resets the layer's references, not the state the earlier records advanced).
+    #     A writer with the same keys makes the valid bodies; before each one its
+    #     seqnum / CBC residue / RC4 state is synced to the reader's, as a peer's would be.
+    from tlslite.errors import TLSLocalAlert
+    for suite in SUITES:
+        for ver in VERSIONS:
+            if not valid(suite, ver):
+                continue
+            tag = "open/%s/%d.%d" % (suite, ver[0], ver[1])
+            keys = mk_keys(tag, suite, seq=77)
+            w = make_layer(suite, ver, keys)
+            r = make_layer(suite, ver, keys)
+            rs = r._writeState  # becomes the reader's read state; alerts go out in the clear
+            r._writeState = _ConnectionState()
+            ws = w._writeState
+            bs = 1 if SUITES[suite][0] == "rc4" else (8 if SUITES[suite][0] == "3des" else 16)
+            plan = [("valid", 40), ("empty", 0), ("raw", bs), ("valid", 1), ("raw", 2 * bs + 1),
+                    ("raw", 4 * bs if bs > 1 else 64), ("valid", 300), ("flip", 70), ("raw", 3),
+                    ("valid", 17), ("flip", 1), ("valid", 1434)]
+            bodies = []
+            for i, (kind, n) in enumerate(plan):
+                if kind in ("valid", "flip"):
+                    ws.seqnum = rs.seqnum
+                    if bs == 1:
+                        ws.encContext.S = list(rs.encContext.S)
+                        ws.encContext.i, ws.encContext.j = rs.encContext.i, rs.encContext.j
+                    elif ver < (3, 2):
+                        ws.encContext.IV = bytearray(rs.encContext.IV)
+                    body = bytearray(seal_records(w, [gen_bytes("%s/pt%d" % (tag, i), n)])[0][5:])
+                    if kind == "flip":
+                        body[len(body) // 2] ^= 0x10
+                else:
+                    body = bytearray(gen_bytes("%s/raw%d" % (tag, i), n))
+                entry = {"type": 23, "body": bytes(body).hex()}
+                r.version, r.closed, r._readState, r._writeState = ver, False, rs, _ConnectionState()
+                try:
+                    out = None
+                    for out in r._decryptRecord(23, bytearray(body)):
+                        pass
+                    entry["status"] = 0
+                    entry["pt"] = bytes(out).hex()
+                except TLSLocalAlert as e:
+                    entry["status"] = e.description
+                bodies.append(entry)
+            enc = rs.encContext
+            fin = {"seqnum": rs.seqnum}
+            if bs == 1:
+                fin.update(rc4_i=enc.i, rc4_j=enc.j, rc4_S=bytes(enc.S).hex())
+            else:
+                fin["cbc_iv"] = bytes(enc.IV).hex()
+            cases.append({"kind": "open", "name": tag, "suite": suite, "version": list(ver), **keys,
+                          "bodies": bodies, "final": fin})
     # (vi) key-block derivation as _calcPendingStates does it (tlsrecordlayer.py:1097-1126):
     #      master secret (mathtls.py:70-82) -> PRF/PRF_1_2/PRF_SSL key block -> slices
     suite_ids = {"AES128-SHA": CipherSuite.TLS_RSA_WITH_AES_128_CBC_SHA,

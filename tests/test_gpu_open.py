@@ -124,3 +124,88 @@ def test_parse_records_overflow():
     assert recs == [(23, (3, 3), b"ab")] and rest == b"\x17\x03"
     with pytest.raises(RecordOverflow):
         parse_records(b"\x17\x03\x03\x48\x01" + bytes(10))
+
+
+@pytest.mark.parametrize("suite", ["AES128-SHA", "AES256-SHA256", "3DES-SHA", "RC4-MD5"])
+@pytest.mark.parametrize("version", [(3, 0), (3, 1), (3, 2), (3, 3)])
+def test_malformed_chains_like_oracle(suite, version):
+    """Chains mixing valid records with empty, IV-only, random-garbage and
+    non-block-multiple bodies (tlsrecordlayer.py:964-977: b[bs:] of a body no
+    longer than one block is empty -> decryption_failed): every status and the
+    final seqnum / CBC residue / RC4 state equal the oracle's."""
+    from oracle import oracle as O
+    from tlslite_amd import _native as N
+    from tlslite_amd.recordlayer import open_records
+    T = _T()
+    if suite.endswith("SHA256") and version != (3, 3):
+        pytest.skip("TLS 1.2 only")
+    rng = np.random.default_rng(zlib.crc32(repr(("malformed", suite, version)).encode()))
+    bs = {"aes128": 16, "aes256": 16, "3des": 8, "rc4": 1}[O.SUITES[suite][0]]
+    readers, oreaders, recs = [], [], []
+    for ci in range(16):
+        mk_t, mk_o = _mk(T, O, suite, version, rng)
+        w_o = mk_o()
+        readers.append(mk_t())
+        oreaders.append(mk_o())
+        for k in range(6):
+            kind = int(rng.integers(0, 5))
+            if kind == 0:
+                body = b""
+            elif kind == 1:
+                body = rng.bytes(bs)
+            elif kind == 2:
+                body = rng.bytes(bs * int(rng.integers(2, 8)))
+            elif kind == 3:
+                body = rng.bytes(bs * 3 + (1 if bs > 1 else 0))
+            else:
+                body = w_o.seal(rng.bytes(int(rng.integers(1, 200))), 23)[5:]
+            recs.append((ci, 23, body))
+    res = open_records(readers, recs)
+    amap = {0: 0, O.ALERT_BAD_RECORD_MAC: N.ALERT_BAD_RECORD_MAC,
+            O.ALERT_DECRYPTION_FAILED: N.ALERT_DECRYPTION_FAILED}
+    for (ci, ct, body), (st, p) in zip(recs, res):
+        ost, opt = oreaders[ci].open(body, ct)
+        assert st == amap[ost], (ci, len(body))
+        if st == 0:
+            assert p == opt
+    for r, o in zip(readers, oreaders):
+        assert r.seqnum == o.seqnum
+        if O.SUITES[suite][0] == "rc4":
+            assert r.rc4 == o.rc4
+        else:
+            assert r.iv == o.iv
+
+
+def test_golden_open_chains(golden):
+    """The reference's _decryptRecord statuses / plaintexts / final state over
+    chains of valid, tampered and malformed bodies (tests/golden open cases),
+    all chains in one open_records call per variant."""
+    from tlslite_amd import _native as N
+    from tlslite_amd.recordlayer import open_records
+    T = _T()
+    amap = {0: 0, 20: N.ALERT_BAD_RECORD_MAC, 21: N.ALERT_DECRYPTION_FAILED}
+    states, recs, expect, cases = [], [], [], []
+    for c in golden:
+        if c["kind"] != "open":
+            continue
+        key, iv, mk, fiv, seq = case_keys(c)
+        si = len(states)
+        states.append(T.ConnectionState.for_suite(c["suite"], tuple(c["version"]), key, iv, mk, fiv, seq))
+        cases.append(c)
+        for b in c["bodies"]:
+            recs.append((si, b["type"], bytes.fromhex(b["body"])))
+            expect.append((amap[b["status"]], bytes.fromhex(b["pt"]) if b["status"] == 0 else None))
+    assert len(cases) == 22
+    res = open_records(states, recs)
+    for (st, pt), (est, ept) in zip(res, expect):
+        assert st == est
+        if est == 0:
+            assert pt == ept
+    for s, c in zip(states, cases):
+        f = c["final"]
+        assert s.seqnum == f["seqnum"], c["name"]
+        if "cbc_iv" in f:
+            assert s.iv.hex() == f["cbc_iv"], c["name"]
+        else:
+            S, i, j = s.rc4
+            assert (S.hex(), i, j) == (f["rc4_S"], f["rc4_i"], f["rc4_j"]), c["name"]

@@ -4,6 +4,7 @@ tlslite (tests/golden/records.json).  CPU only."""
 import hashlib
 import hmac
 
+import numpy as np
 import pytest
 
 from oracle import oracle as O
@@ -137,3 +138,46 @@ def test_open_roundtrip_and_tamper(golden):
                 assert st == O.ALERT_BAD_RECORD_MAC, case["name"]
                 break
             assert st == 0 and pt == rec_pt(rec), case["name"]
+
+
+def test_open_short_bodies_decryption_failed():
+    """tlsrecordlayer.py:964-977: a block-cipher body that is not a block
+    multiple, or leaves nothing after decryption and explicit-IV removal, is
+    decryption_failed; no seqnum is consumed; a decrypted IV-only block still
+    advances the CBC residue (python_aes.py decrypt keeps the last block)."""
+    rng = np.random.default_rng(7)
+    for version in [(3, 0), (3, 1), (3, 2), (3, 3)]:
+        key, iv, mk, fiv = rng.bytes(16), rng.bytes(16), rng.bytes(20), rng.bytes(16)
+        c = O.Conn.for_suite("AES128-SHA", version, key, iv, mk, fiv, 5)
+        for body in (b"", bytes(15)):
+            assert c.open(body, 23)[0] == O.ALERT_DECRYPTION_FAILED
+            assert c.seqnum == 5 and c.iv == iv
+        blk = rng.bytes(16)
+        st, _ = c.open(blk, 23)
+        assert c.iv == blk
+        if version >= (3, 2):
+            assert st == O.ALERT_DECRYPTION_FAILED and c.seqnum == 5
+
+
+def _open_expect(b):
+    return {0: 0, 20: O.ALERT_BAD_RECORD_MAC, 21: O.ALERT_DECRYPTION_FAILED}[b["status"]]
+
+
+def test_golden_open_chains(golden):
+    """Reference _decryptRecord (tlsrecordlayer.py:958-1044) on chains of valid,
+    tampered, empty, IV-only, non-block-multiple and garbage bodies: the oracle
+    reproduces every status, plaintext and the final seqnum / residue / RC4 state."""
+    n = 0
+    for case in golden:
+        if case["kind"] != "open":
+            continue
+        key, iv, mk, fiv, seq = case_keys(case)
+        c = O.Conn.for_suite(case["suite"], tuple(case["version"]), key, iv, mk, fiv, seq)
+        for b in case["bodies"]:
+            st, pt = c.open(bytes.fromhex(b["body"]), b["type"])
+            assert st == _open_expect(b), (case["name"], b)
+            if st == 0:
+                assert pt.hex() == b["pt"], case["name"]
+        _check_final(c, case)
+        n += 1
+    assert n == 22

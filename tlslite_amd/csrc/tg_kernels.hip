@@ -338,7 +338,7 @@ __global__ void __launch_bounds__(SEAL_BLOCK) open_kernel(const tlsgpu_chain* __
                     if (BS == 16) store16(Pb + off - E, d); else store8(Pb + off - E, d);
                 }
             }
-            len = L - E;  // :970-971
+            len = L > E ? L - E : 0u;  // :970-971 (b[E:] of a shorter b is empty)
             if (len == 0) {  // :973-977
                 status[ch.first + k] = TLSGPU_ALERT_DECRYPTION_FAILED;
                 continue;
