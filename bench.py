@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--records", type=int, default=None, help="override record count (debug)")
     ap.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline")
     ap.add_argument("--no-check", action="store_true", help="skip the full-batch parity check")
+    ap.add_argument("--no-open", dest="open", action="store_false", help="skip the open-path measurement")
     ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false",
                     help="skip the PCIe-inclusive measurement (profiling runs)")
     ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
@@ -148,6 +149,36 @@ def host_inclusive_rate(wl, nsub=16):
             "method": "pinned hipMemcpyAsync H2D(plaintext) + seal + D2H(wire), %d sub-batches on 3 streams" % len(subs)}
 
 
+def open_rate(wl, stream, steps):
+    """Open path on the batch: seal once from the initial states, then open it
+    with read states reset to the initial ones before every (timed) call."""
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import Event
+    wl.reset_states(stream)
+    wl.launch([stream])
+    wl.open_setup()
+    wl.open_launch(stream)
+    stream.synchronize()
+    status = wl.d_ostatus.download().view(np.int32)
+    ok = bool(np.array_equal(status, wl.pt_len.astype(np.int32)))
+    if ok:
+        ok = bool(np.array_equal(wl.d_opt.download(), wl.d_pt.download()))
+    ms = []
+    for _ in range(max(1, min(steps, 20))):
+        a, b = Event(), Event()
+        N.call("tlsgpu_memcpy_d2d", wl.d_ostates.ptr, wl.d_states0.ptr, wl.d_ostates.nbytes, stream.handle)
+        a.record(stream)
+        wl.open_launch(stream, reset=False)
+        b.record(stream)
+        stream.synchronize()
+        ms.append(a.elapsed_ms(b))
+    t = float(np.median(ms))
+    return {"value": round(wl.plaintext_total / GIB / (t / 1e3), 2), "unit": "GiB/s", "ms": round(t, 4),
+            "roundtrip_exact": ok,
+            "method": "tlsgpu_open_dev over the sealed batch (AES: block-parallel CBC decrypt, per-chain "
+                      "padding/seqnum pass, per-record MAC verify); median of HIP-event-timed calls"}
+
+
 def main():
     args = parse()
     from tlslite_amd.shard import ShardGroup
@@ -229,6 +260,15 @@ def main():
         except Exception:
             traffic = None
 
+    # ---- open direction (decrypt + padding + MAC verify) of one sealed batch:
+    # round trip checked byte-for-byte against the plaintext arena
+    open_res = None
+    if D.world == 1 and args.open:
+        try:
+            open_res = open_rate(wl, stream, args.steps)
+        except Exception as e:  # reported, never silently replaced
+            open_res = {"error": str(e)}
+
     host_inc = None
     if D.world == 1 and args.host_inclusive:
         try:
@@ -263,6 +303,7 @@ def main():
             "cpu_baseline": cpu,
             "bit_exact": bit_exact,
             "host_inclusive": host_inc,
+            "open": open_res,
         }
         print(json.dumps(out))
     D.close()

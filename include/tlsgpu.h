@@ -207,10 +207,15 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain *chains, uint32_t
                          tlsgpu_conn_state *states, int32_t *wire_len, uint32_t variant,
                          tlsgpu_event cipher_start, tlsgpu_event cipher_stop);
 
-/* status[r] = plaintext length, or TLSGPU_ALERT_* */
+/* Batch open: status[r] = plaintext length, or TLSGPU_ALERT_* (records 0..nrecords-1;
+ * a chain's records open in order on its state, as successive _decryptRecord calls).
+ * AES suites decrypt every block of every record in parallel and need a workspace of
+ * tlsgpu_open_workspace_bytes(nrecords) bytes (NULL = library-owned). */
+size_t tlsgpu_open_workspace_bytes(uint32_t nrecords);
 int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_open_record *records,
-                    const uint8_t *wire, uint8_t *pt, tlsgpu_conn_state *states, int32_t *status,
-                    uint32_t variant, tlsgpu_stream s);
+                    uint32_t nrecords, const uint8_t *wire, uint8_t *pt, tlsgpu_conn_state *states,
+                    int32_t *status, uint32_t variant, void *workspace, size_t workspace_bytes,
+                    tlsgpu_stream s);
 /* raw stateful encrypt (decrypt=0) / decrypt (decrypt=1) of spans; one span
  * per state per launch (a state's spans in one launch run in array order). */
 int tlsgpu_cipher_dev(const tlsgpu_span *spans, uint32_t nspans, const uint8_t *in, uint8_t *out,

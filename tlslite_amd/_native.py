@@ -85,7 +85,8 @@ SIGNATURES = [
     ("tlsgpu_pipeline_destroy", _i, [_vp]),
     ("tlsgpu_pipeline_synchronize", _i, [_vp]),
     ("tlsgpu_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp]),
-    ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    ("tlsgpu_open_workspace_bytes", _sz, [_u32]),
+    ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
     ("tlsgpu_cipher_dev", _i, [_vp, _u32, _vp, _vp, _vp, _i, _i, _vp]),
     ("tlsgpu_fill_pattern", _i, [_vp, _sz, _u64, _u64, _vp]),
 ]

@@ -401,6 +401,30 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state* st, uint32_t pt_len, uint32_t*
 
 size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords) { return seal_workspace_bytes(nrecords); }
 
+// library-owned workspace: per device and per kind, grow-only (calls that use it must not
+// run concurrently on several streams: pass a workspace for that)
+static int own_workspace(int kind, size_t need, uint8_t** out) {
+    static thread_local void* own[2][64] = {{nullptr}};
+    static thread_local size_t own_bytes[2][64] = {{0}};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    dev &= 63;
+    if (own_bytes[kind][dev] < need) {
+        if (own[kind][dev]) TG_HIP(hipFree(own[kind][dev]));
+        own[kind][dev] = nullptr;
+        own_bytes[kind][dev] = 0;
+        TG_HIP(hipMalloc(&own[kind][dev], need));
+        own_bytes[kind][dev] = need;
+    }
+    *out = static_cast<uint8_t*>(own[kind][dev]);
+    return 0;
+}
+
+static uint32_t next_epoch() {
+    static uint32_t epoch_ctr = 0;
+    return __atomic_add_fetch(&epoch_ctr, 1, __ATOMIC_RELAXED);
+}
+
 int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* records, uint32_t nrecords,
                     const uint8_t* pt, uint8_t* wire, tlsgpu_conn_state* states, int32_t* wire_len, uint32_t variant,
                     void* workspace, size_t workspace_bytes, tlsgpu_stream s) {
@@ -410,27 +434,14 @@ int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_r
     if (seal_needs_workspace(variant)) {
         const size_t need = seal_workspace_bytes(nrecords);
         if (ws && workspace_bytes < need) return fail(TLSGPU_EINVAL, "workspace too small");
-        if (!ws) {  // library-owned, per device, grow-only (not for concurrent calls on several streams)
-            static thread_local void* own[64] = {nullptr};
-            static thread_local size_t own_bytes[64] = {0};
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            dev &= 63;
-            if (own_bytes[dev] < need) {
-                if (own[dev]) TG_HIP(hipFree(own[dev]));
-                own[dev] = nullptr;
-                own_bytes[dev] = 0;
-                TG_HIP(hipMalloc(&own[dev], need));
-                own_bytes[dev] = need;
-            }
-            ws = static_cast<uint8_t*>(own[dev]);
+        if (!ws) {
+            int rc = own_workspace(0, need, &ws);
+            if (rc) return rc;
         }
     }
-    static uint32_t epoch_ctr = 0;
-    const uint32_t epoch = __atomic_add_fetch(&epoch_ctr, 1, __ATOMIC_RELAXED);
     bool known = false;
-    hipError_t e = launch_seal(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len, ws, epoch,
-                               HS(s), &known);
+    hipError_t e = launch_seal(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len, ws,
+                               next_epoch(), HS(s), &known);
     if (!known) return fail(TLSGPU_EINVAL, "unsupported seal variant");
     if (e != hipSuccess) return fail_hip(e, "seal launch");
     return 0;
@@ -529,13 +540,25 @@ int tlsgpu_cipher_dev(const tlsgpu_span* spans, uint32_t nspans, const uint8_t* 
     return 0;
 }
 
+size_t tlsgpu_open_workspace_bytes(uint32_t nrecords) { return open_workspace_bytes(nrecords); }
+
 int tlsgpu_open_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* records,
-                    const uint8_t* wire, uint8_t* pt, tlsgpu_conn_state* states, int32_t* status, uint32_t variant,
-                    tlsgpu_stream s) {
+                    uint32_t nrecords, const uint8_t* wire, uint8_t* pt, tlsgpu_conn_state* states, int32_t* status,
+                    uint32_t variant, void* workspace, size_t workspace_bytes, tlsgpu_stream s) {
     if (nchains == 0) return 0;
     if (!chains || !records || !wire || !pt || !states || !status) return fail(TLSGPU_EINVAL, "null pointer");
+    uint8_t* ws = static_cast<uint8_t*>(workspace);
+    if (open_needs_workspace(variant)) {
+        const size_t need = open_workspace_bytes(nrecords);
+        if (ws && workspace_bytes < need) return fail(TLSGPU_EINVAL, "workspace too small");
+        if (!ws) {
+            int rc = own_workspace(1, need, &ws);
+            if (rc) return rc;
+        }
+    }
     bool known = false;
-    hipError_t e = launch_open(variant, chains, nchains, records, wire, pt, S(states), status, HS(s), &known);
+    hipError_t e = launch_open(variant, chains, nchains, records, nrecords, wire, pt, S(states), status, ws,
+                               next_epoch(), HS(s), &known);
     if (!known) return fail(TLSGPU_EINVAL, "unsupported open variant");
     if (e != hipSuccess) return fail_hip(e, "open launch");
     return 0;

@@ -5,9 +5,11 @@
 //                  cipher-object surface (python_aes.py:20-69, python_rc4.py:25-41)
 //   fill_kernel    deterministic synthetic input (splitmix64 byte stream)
 #include <stdlib.h>
+#include <string.h>
 #include "tg_device.h"
 #include "tg_aesq.h"
 #include "tg_aes3.h"
+#include "tg_open3.h"
 #include "tg_launch.h"
 
 namespace tg {
@@ -405,9 +407,9 @@ static hipError_t launch_open_t(const tlsgpu_chain* chains, uint32_t n, const tl
     return hipGetLastError();
 }
 
-hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
-                       const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s,
-                       bool* known) {
+static hipError_t launch_open_lane(uint32_t variant, const tlsgpu_chain* chains, uint32_t n,
+                                   const tlsgpu_open_record* recs, const uint8_t* wire, uint8_t* pt,
+                                   ConnState* states, int32_t* status, hipStream_t s, bool* known) {
     *known = true;
 #define TG_OPEN_CASE(CIPHER_ID, MAC_ID, SSL3)                                                  \
     if (variant == TLSGPU_VARIANT(CIPHER_ID, MAC_ID, SSL3))                                    \
@@ -692,6 +694,66 @@ hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, 
     if (threads == 0) return hipSuccess;
     hipLaunchKernelGGL(fill_kernel, grid, dim3(256), 0, s, p, bytes, seed, start);
     return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------- block-parallel AES open
+size_t open_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * sizeof(OpenMeta); }
+
+static bool open_split_variant(uint32_t v) {
+    const uint32_t c = v & 0xff, m = (v >> 8) & 0xff, ssl3 = (v >> 16) & 1;
+    const bool aes = c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256;
+    return aes && (m == TLSGPU_MAC_SHA1 || (m == TLSGPU_MAC_SHA256 && !ssl3)) && !(getenv("TLSGPU_OPEN_IMPL") &&
+                                                                                   !strcmp(getenv("TLSGPU_OPEN_IMPL"), "lane"));
+}
+bool open_needs_workspace(uint32_t variant) { return open_split_variant(variant); }
+
+template <int NR, int MAC, bool SSL3>
+static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* recs,
+                                    uint32_t nrecords, const uint8_t* wire, uint8_t* pt, ConnState* states,
+                                    int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s) {
+    constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : TLSGPU_CIPHER_AES256;
+    OpenMeta* meta = reinterpret_cast<OpenMeta*>(ws);
+    hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(OpenMeta), s);
+    if (e != hipSuccess) return e;
+    const dim3 gc((nchains + 255) / 256), gr((nrecords + 255) / 256);
+    hipLaunchKernelGGL((open_prefix_kernel<CID, MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords,
+                       wire, states, status, meta, epoch);
+    auto dec = open_dec_kernel<NR>;
+    static bool attr = false;
+    if (!attr) {
+        if ((e = set_lds(dec, AES_DEC_LDS_BYTES)) != hipSuccess) return e;
+        attr = true;
+    }
+    uint32_t grid = (nrecords + (O3_THREADS / 64) - 1) / (O3_THREADS / 64);
+    grid = grid > (uint32_t)cu_count() ? (uint32_t)cu_count() : (grid ? grid : 1u);
+    hipLaunchKernelGGL(dec, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s, recs, nrecords, wire, pt, states, meta,
+                       epoch);
+    hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords, pt, states,
+                       status, meta, epoch);
+    hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status, meta,
+                       epoch);
+    return hipGetLastError();
+}
+
+hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
+                       const tlsgpu_open_record* recs, uint32_t nrecords, const uint8_t* wire, uint8_t* pt,
+                       ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known) {
+    if (open_split_variant(variant)) {
+        *known = true;
+#define TG_OPEN3(CID, NR, MAC_ID, SSL3)                                                                         \
+        if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3))                                                       \
+            return launch_open_split<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, wire, pt, states, status, \
+                                                        ws, epoch, s);
+        TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)
+        TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, false)
+        TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA256, false)
+        TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false)
+        TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)
+        TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)
+#undef TG_OPEN3
+    }
+    return launch_open_lane(variant, chains, nchains, recs, wire, pt, states, status, s, known);
 }
 
 }  // namespace tg

@@ -19,9 +19,11 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
                               bool* known);
 hipError_t launch_cipher(int cipher, int dec, const tlsgpu_span* spans, uint32_t n, const uint8_t* in, uint8_t* out,
                          ConnState* states, hipStream_t s, bool* known);
-hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
-                       const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s,
-                       bool* known);
+size_t open_workspace_bytes(uint32_t nrecords);
+bool open_needs_workspace(uint32_t variant);
+hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
+                       const tlsgpu_open_record* recs, uint32_t nrecords, const uint8_t* wire, uint8_t* pt,
+                       ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known);
 hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, hipStream_t s);
 
 }  // namespace tg

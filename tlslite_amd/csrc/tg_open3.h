@@ -1,0 +1,273 @@
+// tg_open3.h -- block-parallel AES record open (the AES open path).
+//
+// _decryptRecord (tlsrecordlayer.py:958-1044) per record is: CBC-decrypt the
+// body, drop the explicit IV, check the padding, compute the MAC with the next
+// seqnum, compare.  Only the seqnum and the CBC residue are serial per
+// connection, and CBC *decryption* is parallel over blocks (P_i = D(C_i) ^ C_{i-1},
+// every C known up front), so the open path is four launches:
+//
+//   open_prefix_kernel  one lane per chain: length checks (:964-977), the
+//                       predecessor ciphertext block of every record's first
+//                       block, the connection's new residue.
+//   open_dec_kernel     16 waves per CU, 4 lanes per block (AES state column per
+//                       lane, DPP quad exchange), two blocks per quad; waves
+//                       walk records, 32 blocks of one record per step --
+//                       every block of every record in parallel.
+//   open_seq_kernel     one lane per chain: padding check (:979-993) on the
+//                       decrypted tail, which decides whether the MAC is
+//                       computed and so whether a seqnum is consumed (:1018).
+//   open_mac_kernel     one lane per record: MAC over the plaintext, compare
+//                       (:1006-1039), status.
+//
+// Workspace per record: one 48-byte OpenMeta.
+#pragma once
+#include "tg_aesq.h"
+
+namespace tg {
+
+struct OpenMeta {
+    uint32_t pred[4];  // ciphertext block before this record's first block (CBC residue)
+    uint64_t seq;
+    uint32_t state;
+    uint32_t epoch;
+    uint32_t flags;  // OM_*
+    uint32_t len;    // plaintext length after explicit-IV removal
+    uint32_t n;      // payload length (len - MAC - padding)
+    uint32_t pad;
+};
+static_assert(sizeof(OpenMeta) == 48, "OpenMeta");
+constexpr uint32_t OM_DEC = 1, OM_VERIFY = 2, OM_PADOK = 4;
+constexpr int O3_THREADS = 1024;
+
+// Equivalent inverse cipher on the quad layout (FIPS-197 5.3.5, rijndael.py:321-362):
+// column q of the next state = Td0[b0(q)] ^ Td1[b1(q-1)] ^ Td2[b2(q-2)] ^ Td3[b3(q-3)] ^ dk[q];
+// lane q's byte-b lookup feeds column q+b, i.e. lane i takes its term b from lane i-b.
+struct QuadAesDec {
+    QuadAes t;  // same LDS addressing as the encryption tables (decrypt fill)
+    uint32_t isb_base;
+    __device__ __forceinline__ void init() {
+        t.init();
+        isb_base = 131072u + (__lane_id() & 31) * 4;
+    }
+    // lane i reads lane i-1 / i-2 within the quad
+    template <int R>
+    __device__ __forceinline__ uint32_t round(uint32_t x, uint32_t k2) const {
+        const uint32_t t2 = t.look<2, 2>(x);
+        const uint32_t t3 = t.look<3, 3>(x);
+        const uint32_t t0 = t.look<0, 0>(x);
+        const uint32_t t1 = t.look<1, 1>(x);
+        const uint32_t u = (t2 ^ k2) ^ quad_dpp<0x93>(t3);
+        const uint32_t z = t0 ^ quad_dpp<0x93>(t1);
+        return z ^ quad_dpp<0x4E>(u);
+    }
+    template <int B>
+    __device__ __forceinline__ uint32_t isb(uint32_t x) const {  // InvS[byte B of x] << 8B
+        const uint32_t idx = __builtin_amdgcn_ubfe(x, 8 * B, 8);
+        return lds_read32(idx * 128u + isb_base) << (8 * B);
+    }
+    __device__ __forceinline__ uint32_t last(uint32_t x, uint32_t k2) const {
+        const uint32_t s2 = isb<2>(x);
+        const uint32_t s3 = isb<3>(x);
+        const uint32_t s0 = isb<0>(x);
+        const uint32_t s1 = isb<1>(x);
+        const uint32_t u = (s2 ^ k2) ^ quad_dpp<0x93>(s3);
+        const uint32_t z = s0 ^ quad_dpp<0x93>(s1);
+        return z ^ quad_dpp<0x4E>(u);
+    }
+    // two independent blocks, interleaved round by round; k as QuadAes::round_keys on dk
+    template <int NR>
+    __device__ __forceinline__ void decrypt2(uint32_t& a, uint32_t& b, const uint32_t* k) const {
+        a ^= k[0];
+        b ^= k[0];
+#pragma unroll
+        for (int r = 1; r < NR; r++) {
+            const uint32_t na = round<0>(a, k[r]);
+            const uint32_t nb = round<0>(b, k[r]);
+            a = na;
+            b = nb;
+        }
+        const uint32_t la = last(a, k[NR]);
+        const uint32_t lb = last(b, k[NR]);
+        a = la;
+        b = lb;
+    }
+};
+
+template <int CIPHER_ID, int MAC, bool SSL3>
+__global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
+                                                         const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
+                                                         const uint8_t* __restrict__ wire,
+                                                         ConnState* __restrict__ states, int32_t* __restrict__ status,
+                                                         OpenMeta* __restrict__ meta, uint32_t epoch) {
+    const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cid >= nchains) return;
+    const tlsgpu_chain ch = chains[cid];
+    ConnState* st = states + ch.state;
+    const bool ok = st->cipher == (uint32_t)CIPHER_ID && st->mac == (uint32_t)MAC &&
+                    st->ssl3 == (SSL3 ? 1u : 0u) && !st->raw;
+    const uint32_t E = st->explicit_iv ? 16u : 0u;
+    uint32_t res[4] = {st->iv[0], st->iv[1], st->iv[2], st->iv[3]};
+    for (uint32_t k = 0; k < ch.count; k++) {
+        const uint32_t r = ch.first + k;
+        if (r >= nrecords) break;
+        OpenMeta m;
+#pragma unroll
+        for (int i = 0; i < 4; i++) m.pred[i] = res[i];
+        m.seq = 0;
+        m.state = ch.state;
+        m.epoch = epoch;
+        m.flags = 0;
+        m.len = 0;
+        m.n = 0;
+        m.pad = 0;
+        if (!ok) {
+            status[r] = TLSGPU_EMISMATCH;
+        } else {
+            const tlsgpu_open_record R = recs[r];
+            const uint32_t L = R.ct_len;
+            if (L & 15u) {  // :964-968 -- not decrypted, residue unchanged
+                status[r] = TLSGPU_ALERT_DECRYPTION_FAILED;
+            } else {
+                if (L) load16(wire + R.ct_off + L - 16, res);  // decrypt() keeps the last block
+                if (L <= E) {                                  // :970-977 nothing left after the IV
+                    status[r] = TLSGPU_ALERT_DECRYPTION_FAILED;
+                } else {
+                    m.flags = OM_DEC;
+                    m.len = L - E;
+                }
+            }
+        }
+        meta[r] = m;
+    }
+    if (ok) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) st->iv[i] = res[i];
+    }
+}
+
+template <int NR>
+__global__ void __launch_bounds__(O3_THREADS, 1)
+open_dec_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
+                uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
+                uint32_t epoch) {
+    aes_lds_fill(nullptr, true);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t quad = lane >> 2, q = lane & 3;
+    const uint32_t nwaves = gridDim.x * (O3_THREADS / 64);
+    QuadAesDec aes;
+    aes.init();
+    for (uint32_t r = blockIdx.x * (O3_THREADS / 64) + (threadIdx.x >> 6); r < nrecords; r += nwaves) {
+        const OpenMeta& mt = meta[r];
+        if (mt.epoch != epoch || !(mt.flags & OM_DEC)) continue;
+        const ConnState* st = states + mt.state;
+        uint32_t k[NR + 1];
+        QuadAes::round_keys<NR>(st->dk, q, k);
+        const tlsgpu_open_record R = recs[r];
+        const uint32_t E = st->explicit_iv ? 16u : 0u;
+        const uint32_t nb = R.ct_len >> 4;
+        const uint8_t* C = wire + R.ct_off + 4 * q;
+        uint8_t* P = pt + R.pt_off + 4 * q;
+        const bool al = ((R.ct_off | R.pt_off) & 3) == 0;
+        const uint32_t pq = mt.pred[q];
+        for (uint32_t b0 = 0; b0 < nb; b0 += 32) {
+            const uint32_t ba = b0 + quad, bb = b0 + 16 + quad;
+            const bool va = ba < nb, vb = bb < nb;
+            uint32_t ca = va ? ld32(C + 16 * ba, al) : 0u;
+            uint32_t cb = vb ? ld32(C + 16 * bb, al) : 0u;
+            const uint32_t pa = ba == 0 ? pq : (va ? ld32(C + 16 * (ba - 1), al) : 0u);
+            const uint32_t pb = vb ? ld32(C + 16 * (bb - 1), al) : 0u;
+            aes.decrypt2<NR>(ca, cb, k);
+            if (va && 16 * ba >= E) st32(P + 16 * ba - E, ca ^ pa, al);
+            if (vb && 16 * bb >= E) st32(P + 16 * bb - E, cb ^ pb, al);
+        }
+    }
+}
+
+template <int MAC, bool SSL3>
+__global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
+                                                      const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
+                                                      const uint8_t* __restrict__ pt, ConnState* __restrict__ states,
+                                                      int32_t* __restrict__ status, OpenMeta* __restrict__ meta,
+                                                      uint32_t epoch) {
+    constexpr uint32_t DL = Hash<MAC>::DLEN;
+    const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cid >= nchains) return;
+    const tlsgpu_chain ch = chains[cid];
+    ConnState* st = states + ch.state;
+    uint64_t seq = st->seqnum;
+    bool any = false;
+    for (uint32_t k = 0; k < ch.count; k++) {
+        const uint32_t r = ch.first + k;
+        if (r >= nrecords) break;
+        OpenMeta& m = meta[r];
+        if (m.epoch != epoch || !(m.flags & OM_DEC)) continue;
+        any = true;
+        const uint8_t* P = pt + recs[r].pt_off;
+        const uint32_t len = m.len;
+        const uint32_t pl = P[len - 1];
+        bool padGood = true;
+        uint32_t totalPad = 0;
+        if (pl + 1 > len) {  // :981-983
+            padGood = false;
+        } else {
+            totalPad = pl + 1;
+            if (!SSL3) {  // TLS: every padding byte equals the length (:986-993)
+                for (uint32_t i = len - totalPad; i < len - 1; i++)
+                    if (P[i] != pl) padGood = false;
+                if (!padGood) totalPad = 0;
+            }
+        }
+        const uint32_t endLen = DL + totalPad;
+        if (endLen > len) {  // :1006-1007 -- no MAC computed, no seqnum consumed
+            status[r] = TLSGPU_ALERT_BAD_RECORD_MAC;
+            m.flags = 0;
+        } else {
+            m.n = len - endLen;
+            m.seq = seq++;  // getSeqNumBytes (:1018)
+            m.flags = OM_DEC | OM_VERIFY | (padGood ? OM_PADOK : 0u);
+        }
+    }
+    if (any) st->seqnum = seq;
+}
+
+template <int MAC, bool SSL3>
+__global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
+                                                      const uint8_t* __restrict__ pt,
+                                                      const ConnState* __restrict__ states,
+                                                      int32_t* __restrict__ status,
+                                                      const OpenMeta* __restrict__ meta, uint32_t epoch) {
+    using M = RecMac<MAC, SSL3>;
+    constexpr int DL = M::DL;
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nrecords) return;
+    const OpenMeta mt = meta[r];
+    if (mt.epoch != epoch || !(mt.flags & OM_VERIFY)) return;
+    const ConnState* st = states + mt.state;
+    const tlsgpu_open_record R = recs[r];
+    const uint8_t* P = pt + R.pt_off;
+    const uint32_t n = mt.n;
+    M mac;
+    mac.begin(st, mt.seq, R.content_type, n);
+    const uint32_t nfull = n >> 6;
+    uint32_t nxt[16];
+    if (nfull) load64(P, nxt);
+    for (uint32_t c = 0; c < nfull; c++) {
+        uint32_t cur[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) cur[j] = nxt[j];
+        if (c + 1 < nfull) load64(P + 64 * (c + 1), nxt);
+        mac.update(cur);
+    }
+    uint32_t tail[16];
+    load_partial(P + 64 * nfull, n & 63, tail);
+    uint32_t m[8];
+    mac.finish(tail, (int)(n & 63), n, st, m);
+    bool macGood = true;
+#pragma unroll
+    for (int i = 0; i < DL; i++)
+        if (P[n + i] != (uint8_t)(m[i >> 2] >> (8 * (i & 3)))) macGood = false;
+    status[r] = ((mt.flags & OM_PADOK) && macGood) ? (int32_t)n : TLSGPU_ALERT_BAD_RECORD_MAC;
+}
+
+}  // namespace tg

@@ -262,11 +262,17 @@ def make_open_records(ct_off, pt_off, ct_len, content_type):
     return recs
 
 
-def open_dev(chains, nchains, records, wire, pt, states, status, variant, stream=None):
-    """Device-resident batch open (decrypt + padding + MAC check)."""
+def open_workspace_bytes(nrecords):
+    return int(N.lib.tlsgpu_open_workspace_bytes(int(nrecords)))
+
+
+def open_dev(chains, nchains, records, nrecords, wire, pt, states, status, variant, workspace=None, stream=None):
+    """Device-resident batch open (decrypt + padding + MAC check).  workspace:
+    DeviceBuffer of >= open_workspace_bytes(nrecords), or None (library-owned)."""
     def p(x):
         return x.ptr if isinstance(x, DeviceBuffer) else ctypes.c_void_p(x)
-    N.call("tlsgpu_open_dev", p(chains), nchains, p(records), p(wire), p(pt), p(states), p(status), variant,
+    N.call("tlsgpu_open_dev", p(chains), nchains, p(records), int(nrecords), p(wire), p(pt), p(states), p(status),
+           variant, None if workspace is None else p(workspace), 0 if workspace is None else workspace.nbytes,
            stream.handle if stream is not None else None)
 
 
@@ -320,7 +326,7 @@ def open_records(states, records, stream=None):
         d_ch = DeviceBuffer(ctypes.sizeof(c))
         d_ch.upload(np.frombuffer(c, dtype=np.uint8), stream=stream)
         keep.append(d_ch)
-        open_dev(d_ch, len(chs), d_recs, d_ct, d_pt, d_states, d_st, var, stream)
+        open_dev(d_ch, len(chs), d_recs, nrec, d_ct, d_pt, d_states, d_st, var, stream=stream)
     if stream is not None:
         stream.synchronize()
     pt_host = d_pt.download()

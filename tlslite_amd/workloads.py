@@ -22,7 +22,7 @@ import numpy as np
 from . import _native as N
 from .constants import ContentType, suite_primitives
 from .device import DeviceBuffer, fill_pattern
-from .recordlayer import make_chains, make_records
+from .recordlayer import make_chains, make_open_records, make_records, open_dev, open_workspace_bytes
 from .state import STATE_BYTES, ConnectionState
 
 
@@ -212,6 +212,30 @@ class Workload:
             N.call("tlsgpu_seal_dev", d_ch.ptr, nch, self.d_recs.ptr, self.n_records, self.d_pt.ptr, self.d_wire.ptr,
                    self.d_states.ptr, self.d_len.ptr, var, ws.ptr, ws.nbytes, s.handle if s else None)
 
+    # ------------------------------------------------------------ open direction
+    def open_setup(self):
+        """Open descriptors for the sealed wire arena: record r's body at
+        wire_off+5, its plaintext back to pt_off of a second arena; read states
+        start from the initial states (what the peer's read side holds)."""
+        body = np.clip(self.wire_len - 5, 0, None)
+        recs = make_open_records(self.wire_off + 5, self.pt_off, body, ContentType.application_data)
+        self.d_orecs = DeviceBuffer(ctypes.sizeof(recs))
+        self.d_orecs.upload(np.frombuffer(recs, dtype=np.uint8))
+        self.d_opt = DeviceBuffer(self.pt_bytes)
+        self.d_ostatus = DeviceBuffer(4 * self.n_records)
+        self.d_ostates = DeviceBuffer(self.d_states0.nbytes)
+        self.d_ows = DeviceBuffer(max(open_workspace_bytes(self.n_records), 16))
+        return self
+
+    def open_launch(self, stream=None, reset=True):
+        """Open every record of the wire arena once (one call per variant)."""
+        if reset:
+            N.call("tlsgpu_memcpy_d2d", self.d_ostates.ptr, self.d_states0.ptr, self.d_ostates.nbytes,
+                   stream.handle if stream else None)
+        for var, d_ch, nch in self.launches:
+            open_dev(d_ch, nch, self.d_orecs, self.n_records, self.d_wire, self.d_opt, self.d_ostates,
+                     self.d_ostatus, var, self.d_ows, stream)
+
     def dominant_kernel(self):
         """Name (rocprof stem) of the kernel that dominates the first launch."""
         var = self.launches[0][0]
@@ -221,7 +245,8 @@ class Workload:
         return "seal_kernel"
 
     def free(self):
-        for name in ("d_pt", "d_wire", "d_len", "d_recs", "d_states", "d_states0"):
+        for name in ("d_pt", "d_wire", "d_len", "d_recs", "d_states", "d_states0", "d_orecs", "d_opt", "d_ostatus",
+                     "d_ostates", "d_ows"):
             b = getattr(self, name, None)
             if b is not None:
                 b.free()
