@@ -250,4 +250,224 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
     if (any) st->iv[q] = iv;
 }
 
+// ---------------------------------------------------------------------------
+// cbc2_kernel: 8 waves x 16 quads, TWO chains per quad (ILP 2): the bulk blocks
+// of the two chains' current records are encrypted interleaved round by round;
+// explicit-IV and tail blocks (a few per record) run one chain at a time.  Same
+// results as cbc_kernel; chosen when a CU holds more chains than one wave's
+// issue slots can keep in flight (TLSGPU_CBC_ILP selects explicitly).
+struct CbcCur {
+    const tlsgpu_chain* ch;
+    uint32_t first, count, j;  // chain records, next record index
+    uint32_t r, n, nb, b, T, E;
+    const uint8_t* P;
+    uint8_t* O;
+    uint8_t* Ot;
+    const uint8_t* slot;
+    bool al, active, done, any;
+    uint32_t iv, fiv;
+};
+
+template <int NR>
+struct Cbc2 {
+    const tlsgpu_record* recs;
+    const RecMeta* meta;
+    const uint8_t* pt;
+    uint8_t* wire;
+    const uint8_t* tails;
+    uint32_t nrecords, epoch, q, skip_bulk;
+    QuadAes aes;
+
+    // tail blocks of the current record, then inactive
+    __device__ __forceinline__ void finish(CbcCur& c, const uint32_t* k) const {
+        for (uint32_t off = 0; off < c.T; off += 16) {
+            c.iv = aes.encrypt1<NR>(*(const uint32_t*)(c.slot + off) ^ c.iv, k);
+            st32(c.Ot + off, c.iv, c.al);
+        }
+        c.active = false;
+    }
+    // move to the next sealable record: explicit-IV block, bulk cursor; records
+    // without bulk blocks are finished on the spot
+    __device__ __forceinline__ void advance(CbcCur& c, const uint32_t* k) const {
+        while (!c.active && !c.done) {
+            if (c.j >= c.count || c.first + c.j >= nrecords) {
+                c.done = true;
+                break;
+            }
+            const uint32_t r = c.first + c.j++;
+            const RecMeta mt = meta[r];
+            if (mt.epoch != epoch || mt.status != 1) continue;
+            c.any = true;
+            const tlsgpu_record R = recs[r];
+            c.r = r;
+            c.n = R.pt_len;
+            uint8_t* B = wire + R.wire_off + 5;
+            c.al = (((uintptr_t)(pt + R.pt_off) | (uintptr_t)B) & 3) == 0;
+            if (c.E) {
+                c.iv = aes.encrypt1<NR>(c.fiv ^ c.iv, k);
+                st32(B + 4 * q, c.iv, c.al);
+            }
+            c.P = pt + R.pt_off + 4 * q;
+            c.O = B + c.E + 4 * q;
+            c.nb = skip_bulk ? 0u : (c.n >> 4);
+            c.b = 0;
+            const uint32_t r16 = c.n & 15;
+            c.slot = tails + (size_t)r * TAIL_SLOT + 4 * q;
+            c.Ot = B + c.E + (c.n - r16) + 4 * q;
+            c.T = mt.tail_len;
+            c.active = true;
+            if (c.nb == 0) finish(c, k);
+        }
+    }
+    // m bulk blocks of one chain (prefetch 8 ahead)
+    __device__ __forceinline__ void bulk1(CbcCur& c, uint32_t m, const uint32_t* k) const {
+        const uint8_t* P = c.P + 16 * c.b;
+        uint8_t* O = c.O + 16 * c.b;
+        uint32_t f[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) f[i] = (uint32_t)i < m ? ld32(P + 16 * i, c.al) : 0u;
+        for (uint32_t b0 = 0; b0 < m; b0 += 8) {
+            uint32_t x[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) x[i] = f[i];
+#pragma unroll
+            for (int i = 0; i < 8; i++) f[i] = b0 + 8 + i < m ? ld32(P + 16 * (b0 + 8 + i), c.al) : 0u;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                if (b0 + i < m) {
+                    c.iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(x[i], c.iv, k[0], 0x96), k);
+                    st32(O + 16 * (b0 + i), c.iv, c.al);
+                }
+            }
+        }
+        c.b += m;
+    }
+    // m bulk blocks of both chains, interleaved (prefetch 4 ahead each)
+    __device__ __forceinline__ void bulk2(CbcCur& a, const uint32_t* ka, CbcCur& b, const uint32_t* kb,
+                                          uint32_t m) const {
+        const uint8_t* Pa = a.P + 16 * a.b;
+        const uint8_t* Pb = b.P + 16 * b.b;
+        uint8_t* Oa = a.O + 16 * a.b;
+        uint8_t* Ob = b.O + 16 * b.b;
+        uint32_t fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            fa[i] = (uint32_t)i < m ? ld32(Pa + 16 * i, a.al) : 0u;
+            fb[i] = (uint32_t)i < m ? ld32(Pb + 16 * i, b.al) : 0u;
+        }
+        for (uint32_t b0 = 0; b0 < m; b0 += 4) {
+            uint32_t xa[4], xb[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                xa[i] = fa[i];
+                xb[i] = fb[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const bool v = b0 + 4 + i < m;
+                fa[i] = v ? ld32(Pa + 16 * (b0 + 4 + i), a.al) : 0u;
+                fb[i] = v ? ld32(Pb + 16 * (b0 + 4 + i), b.al) : 0u;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                if (b0 + i < m) {
+                    uint32_t ya = __builtin_amdgcn_bitop3_b32(xa[i], a.iv, ka[0], 0x96);
+                    uint32_t yb = __builtin_amdgcn_bitop3_b32(xb[i], b.iv, kb[0], 0x96);
+#pragma unroll
+                    for (int rr = 1; rr < NR; rr++) {
+                        const uint32_t na = aes.round<0>(ya, ka[rr]);
+                        const uint32_t nb2 = aes.round<0>(yb, kb[rr]);
+                        ya = na;
+                        yb = nb2;
+                    }
+                    a.iv = aes.last(ya, ka[NR]);
+                    b.iv = aes.last(yb, kb[NR]);
+                    st32(Oa + 16 * (b0 + i), a.iv, a.al);
+                    st32(Ob + 16 * (b0 + i), b.iv, b.al);
+                }
+            }
+        }
+        a.b += m;
+        b.b += m;
+    }
+};
+
+constexpr int C2_THREADS = 512;  // 8 waves x 16 quads x 2 chains = 256 chains
+
+template <int NR>
+__global__ void __launch_bounds__(C2_THREADS, 1)
+cbc2_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
+            uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
+            ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,
+            uint32_t cpw, uint32_t epoch, uint32_t debug_skip) {
+    aes_lds_fill(nullptr, false);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t local = (threadIdx.x >> 6) * 16 + (lane >> 2);  // 0..127
+    const uint32_t q = lane & 3;
+    const uint32_t half = (cpw + 1) / 2;
+    const uint32_t la = local, lb = local + half;
+    const bool hasA = la < half && blockIdx.x * cpw + la < nchains;
+    const bool hasB = lb < cpw && blockIdx.x * cpw + lb < nchains;
+    if (!hasA) return;
+    set_prio(prio_of(debug_skip, 4, 1));
+    Cbc2<NR> E2;
+    E2.recs = recs;
+    E2.meta = meta;
+    E2.pt = pt;
+    E2.wire = wire;
+    E2.tails = tails;
+    E2.nrecords = nrecords;
+    E2.epoch = epoch;
+    E2.q = q;
+    E2.skip_bulk = debug_skip & 1;
+    E2.aes.init();
+    CbcCur A, B;
+    uint32_t ka[NR + 1], kb[NR + 1];
+    ConnState* sa = states + chains[blockIdx.x * cpw + la].state;
+    ConnState* sb = nullptr;
+    {
+        const tlsgpu_chain c = chains[blockIdx.x * cpw + la];
+        A.first = c.first; A.count = c.count; A.j = 0;
+        A.E = sa->explicit_iv ? 16u : 0u; A.iv = sa->iv[q]; A.fiv = sa->fixed_iv[q];
+        A.active = false; A.done = false; A.any = false;
+        QuadAes::round_keys<NR>(sa->ek, q, ka);
+    }
+    if (hasB) {
+        const tlsgpu_chain c = chains[blockIdx.x * cpw + lb];
+        sb = states + c.state;
+        B.first = c.first; B.count = c.count; B.j = 0;
+        B.E = sb->explicit_iv ? 16u : 0u; B.iv = sb->iv[q]; B.fiv = sb->fixed_iv[q];
+        B.active = false; B.done = false; B.any = false;
+        QuadAes::round_keys<NR>(sb->ek, q, kb);
+    } else {
+        B.done = true; B.active = false; B.any = false;
+#pragma unroll
+        for (int r = 0; r <= NR; r++) kb[r] = 0;
+        B.iv = 0;
+    }
+    E2.advance(A, ka);
+    E2.advance(B, kb);
+    while (A.active || B.active) {
+        if (A.active && B.active) {
+            const uint32_t ra = A.nb - A.b, rb = B.nb - B.b;
+            E2.bulk2(A, ka, B, kb, ra < rb ? ra : rb);
+        } else if (A.active) {
+            E2.bulk1(A, A.nb - A.b, ka);
+        } else {
+            E2.bulk1(B, B.nb - B.b, kb);
+        }
+        if (A.active && A.b == A.nb) {
+            E2.finish(A, ka);
+            E2.advance(A, ka);
+        }
+        if (B.active && B.b == B.nb) {
+            E2.finish(B, kb);
+            E2.advance(B, kb);
+        }
+    }
+    if (A.any) sa->iv[q] = A.iv;
+    if (hasB && B.any) sb->iv[q] = B.iv;
+}
+
 }  // namespace tg

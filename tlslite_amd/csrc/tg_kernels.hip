@@ -518,6 +518,24 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
                                    uint8_t* ws, uint32_t epoch, hipStream_t s) {
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
+    // TLSGPU_CBC_ILP (read per launch): 1 = cbc_kernel (16 waves, 1 chain per quad), 2 = cbc2_kernel
+    // (8 waves, 2 chains per quad)
+    const char* ilp_env = getenv("TLSGPU_CBC_ILP");
+    const int ilp = (ilp_env && atoi(ilp_env) == 2) ? 2 : 1;
+    uint32_t cpw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
+    cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
+    if (ilp == 2) {
+        auto kern = cbc2_kernel<NR>;
+        static bool attr2 = false;
+        if (!attr2) {
+            hipError_t e = set_lds(kern, AES_LDS_BYTES);
+            if (e != hipSuccess) return e;
+            attr2 = true;
+        }
+        hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C2_THREADS), AES_LDS_BYTES, s, chains, nchains,
+                           recs, nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
+        return hipGetLastError();
+    }
     auto kern = cbc_kernel<NR>;
     static bool attr = false;
     if (!attr) {
@@ -525,8 +543,6 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         if (e != hipSuccess) return e;
         attr = true;
     }
-    uint32_t cpw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
-    cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
     hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C3_THREADS), AES_LDS_BYTES, s, chains, nchains, recs,
                        nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
     return hipGetLastError();
