@@ -165,15 +165,19 @@ def test_pipeline_equals_sequential(kind):
     wl.free()
 
 
-@pytest.mark.parametrize("ilp", ["1", "2"])
+@pytest.mark.parametrize("ilp", ["cbc1", "cbc2", "fused", "lane"])
 @pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 1)), ("AES256-SHA256", (3, 3)), ("AES128-SHA", (3, 0))])
 def test_cbc_variants_chained_vs_oracle(ilp, suite, version, monkeypatch):
-    """Both CBC kernels (TLSGPU_CBC_ILP=1: one chain per quad; =2: two chains per
-    quad, bulk interleaved, IV/tail blocks one chain at a time) on chains of
-    mixed record counts and lengths (incl. empty and sub-block records) equal the
-    oracle, including the final CBC residue and seqnum."""
+    """Every AES seal kernel -- split path with cbc_kernel (one chain per quad) or
+    cbc2_kernel (two chains per quad, bulk interleaved, IV/tail blocks one chain
+    at a time), the fused single-kernel path, the 1-lane kernel -- on chains of
+    mixed record counts and lengths (incl. empty and sub-block records) equals
+    the oracle, including the final CBC residue and seqnum."""
     from oracle import oracle as O
-    monkeypatch.setenv("TLSGPU_CBC_ILP", ilp)
+    if ilp.startswith("cbc"):
+        monkeypatch.setenv("TLSGPU_CBC_ILP", ilp[3])
+    else:
+        monkeypatch.setenv("TLSGPU_SEAL_IMPL", ilp)
     T = _T()
     rng = np.random.default_rng(zlib.crc32(repr(("ilp", suite, version)).encode()))
     cipher, kl, ivl, mac, ml = O.SUITES[suite]

@@ -465,13 +465,9 @@ static hipError_t set_lds(K kern, uint32_t bytes) {
 
 // AES implementation: 0 = split (prefix/mac/cbc, default), 1 = fused quad
 // kernel (TLSGPU_SEAL_IMPL=fused), 2 = one lane per chain (=lane).  A/B only.
-static int aes_impl() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("TLSGPU_SEAL_IMPL");
-        v = (e && e[0] == 'f') ? 1 : (e && e[0] == 'l') ? 2 : 0;
-    }
-    return v;
+static int aes_impl() {  // TLSGPU_SEAL_IMPL, read per launch: split (default) / fused / lane
+    const char* e = getenv("TLSGPU_SEAL_IMPL");
+    return (e && e[0] == 'f') ? 1 : (e && e[0] == 'l') ? 2 : 0;
 }
 static uint32_t debug_skip_flags() {
     static uint32_t skip = 0xffffffffu;
