@@ -176,11 +176,14 @@ def test_malformed_chains_like_oracle(suite, version):
             assert r.iv == o.iv
 
 
-def test_golden_open_chains(golden):
+@pytest.mark.parametrize("impl", ["split", "lane"])
+def test_golden_open_chains(golden, impl, monkeypatch):
     """The reference's _decryptRecord statuses / plaintexts / final state over
     chains of valid, tampered and malformed bodies (tests/golden open cases),
-    all chains in one open_records call per variant."""
+    all chains in one open_records call per variant; AES through the
+    block-parallel path (split) and the one-lane-per-chain kernel (lane)."""
     from tlslite_amd import _native as N
+    monkeypatch.setenv("TLSGPU_OPEN_IMPL", impl)
     from tlslite_amd.recordlayer import open_records
     T = _T()
     amap = {0: 0, 20: N.ALERT_BAD_RECORD_MAC, 21: N.ALERT_DECRYPTION_FAILED}
