@@ -162,7 +162,7 @@ def open_rate(wl, stream, steps):
     status = wl.d_ostatus.download().view(np.int32)
     ok = bool(np.array_equal(status, wl.pt_len.astype(np.int32)))
     if ok:
-        ok = bool(np.array_equal(wl.d_opt.download(), wl.d_pt.download()))
+        ok = wl.opened_plaintext_matches()
     ms = []
     for _ in range(max(1, min(steps, 20))):
         a, b = Event(), Event()
@@ -188,6 +188,7 @@ def main():
     if device_count() < 1:
         raise SystemExit("bench.py: no GPU visible to libtlsgpu.so")
     set_device(D.local % device_count())
+    dev_arch = arch(D.local % device_count())
     wl = build_workload(args.config, D.rank, D.world, args.records)
     stream = Stream()
     wl.to_device(stream)
@@ -294,7 +295,7 @@ def main():
             "config": {"workload": wl.name, "records_per_gpu": wl.n_records,
                        "plaintext_bytes_per_gpu": wl.plaintext_total,
                        "parallelism": "connection-sharded x%d (no collective)" % D.world,
-                       "device": arch(D.local % device_count())},
+                       "device": dev_arch},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": wl.dominant_kernel(), "kernel_avg_ms": round(avg_ms, 4),

@@ -209,6 +209,8 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain *chains, uint32_t
 
 /* Batch open: status[r] = plaintext length, or TLSGPU_ALERT_* (records 0..nrecords-1;
  * a chain's records open in order on its state, as successive _decryptRecord calls).
+ * The whole decrypted body after the explicit IV (payload | MAC | padding, ct_len - IV
+ * bytes) is written at pt + pt_off: size the plaintext slots for it.
  * AES suites decrypt every block of every record in parallel and need a workspace of
  * tlsgpu_open_workspace_bytes(nrecords) bytes (NULL = library-owned). */
 size_t tlsgpu_open_workspace_bytes(uint32_t nrecords);

@@ -218,14 +218,27 @@ class Workload:
         wire_off+5, its plaintext back to pt_off of a second arena; read states
         start from the initial states (what the peer's read side holds)."""
         body = np.clip(self.wire_len - 5, 0, None)
-        recs = make_open_records(self.wire_off + 5, self.pt_off, body, ContentType.application_data)
+        # the open path writes the whole decrypted body (payload | MAC | padding) after the
+        # explicit IV: give each record the wire slot's room, 16-byte aligned
+        self.opt_off = (self.wire_off - 11).astype(np.uint64)
+        assert int((self.opt_off + body).max(initial=0)) <= self.wire_bytes
+        recs = make_open_records(self.wire_off + 5, self.opt_off, body, ContentType.application_data)
         self.d_orecs = DeviceBuffer(ctypes.sizeof(recs))
         self.d_orecs.upload(np.frombuffer(recs, dtype=np.uint8))
-        self.d_opt = DeviceBuffer(self.pt_bytes)
+        self.d_opt = DeviceBuffer(self.wire_bytes)
         self.d_ostatus = DeviceBuffer(4 * self.n_records)
         self.d_ostates = DeviceBuffer(self.d_states0.nbytes)
         self.d_ows = DeviceBuffer(max(open_workspace_bytes(self.n_records), 16))
         return self
+
+    def opened_plaintext_matches(self):
+        """Every record's opened payload equals its plaintext (host compare)."""
+        got, ref = self.d_opt.download(), self.d_pt.download()
+        for r in range(self.n_records):
+            n, a, b = int(self.pt_len[r]), int(self.opt_off[r]), int(self.pt_off[r])
+            if not np.array_equal(got[a:a + n], ref[b:b + n]):
+                return False
+        return True
 
     def open_launch(self, stream=None, reset=True):
         """Open every record of the wire arena once (one call per variant)."""
