@@ -174,6 +174,60 @@ __global__ void __launch_bounds__(256) mac_kernel(const tlsgpu_record* __restric
     wire_len[r] = (int32_t)(body + 5);
 }
 
+
+template <bool AL>
+__device__ __forceinline__ uint32_t ld32t(const uint8_t* p) {
+    if constexpr (AL) return *(const uint32_t*)p;
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+template <bool AL>
+__device__ __forceinline__ void st32t(uint8_t* p, uint32_t v) {
+    if constexpr (AL) {
+        *(uint32_t*)p = v;
+    } else {
+        p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+    }
+}
+
+// CBC over nb full plaintext blocks of one chain (P / O include the lane's column offset).
+// Groups of 8 blocks with the next group's columns prefetched; the group loop has no
+// branches and the prefetch index is clamped to the last block (never out of the record),
+// so the compiler's vmcnt waits cover only the loads a block actually consumes -- a
+// conditional load per block made it wait for the whole prefetch (vmcnt(0)) every group.
+template <int NR, bool AL>
+__device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t* k, uint32_t iv,
+                                             const uint8_t* P, uint8_t* O, uint32_t nb) {
+    if (nb == 0) return iv;
+    const uint32_t last = nb - 1;
+    uint32_t f[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) f[i] = ld32t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
+    uint32_t b0 = 0;
+    for (; b0 + 8 <= nb; b0 += 8) {
+        uint32_t c[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) c[i] = f[i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t b = b0 + 8 + i;
+            f[i] = ld32t<AL>(P + 16 * (b < last ? b : last));
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(c[i], iv, k[0], 0x96), k);
+            st32t<AL>(O + 16 * (b0 + i), iv);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        if (b0 + i < nb) {
+            iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(f[i], iv, k[0], 0x96), k);
+            st32t<AL>(O + 16 * (b0 + i), iv);
+        }
+    }
+    return iv;
+}
+
 template <int NR>
 __global__ void __launch_bounds__(C3_THREADS, 1)
 cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
@@ -216,27 +270,7 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
         }
         uint8_t* O = B + E + 4 * q;
         const uint32_t nb = (debug_skip & 1) ? 0u : (n >> 4);
-        // whitening: block ^ previous ciphertext ^ k[0] as one 3-input v_bitop3
-        uint32_t f[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) f[i] = (uint32_t)i < nb ? ld32(P + 16 * i, al) : 0u;
-        for (uint32_t b0 = 0; b0 < nb; b0 += 8) {
-            uint32_t c[8];
-#pragma unroll
-            for (int i = 0; i < 8; i++) c[i] = f[i];
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint32_t b = b0 + 8 + i;
-                f[i] = b < nb ? ld32(P + 16 * b, al) : 0u;
-            }
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                if (b0 + i < nb) {
-                    iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(c[i], iv, k[0], 0x96), k);
-                    st32(O + 16 * (b0 + i), iv, al);
-                }
-            }
-        }
+        iv = al ? cbc_bulk<NR, true>(aes, k, iv, P, O, nb) : cbc_bulk<NR, false>(aes, k, iv, P, O, nb);
         // tail blocks from the MAC kernel's slot
         const uint32_t r16 = n & 15;
         const uint8_t* slot = tails + (size_t)r * TAIL_SLOT + 4 * q;
