@@ -95,6 +95,37 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
     if (ok) st->seqnum = seq;
 }
 
+// 64-byte chunk load: 4 x dwordx4 when 16-byte aligned, else the generic path
+template <bool AL16>
+__device__ __forceinline__ void load64t(const uint8_t* p, uint32_t d[16]) {
+    if constexpr (AL16) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 v = ((const uint4*)p)[q];
+            d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+        }
+    } else {
+        load64(p, d);
+    }
+}
+
+// MAC over nfull 64-byte chunks with the next chunk prefetched; the prefetch index is
+// clamped instead of guarded so the loop body has no branch on the load
+template <bool AL16, class M>
+__device__ __forceinline__ void mac_bulk(M& mac, const uint8_t* P, uint32_t nfull) {
+    if (nfull == 0) return;
+    uint32_t nxt[16];
+    load64t<AL16>(P, nxt);
+    for (uint32_t c = 0; c < nfull; c++) {
+        uint32_t cur[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) cur[j] = nxt[j];
+        const uint32_t cn = c + 1 < nfull ? c + 1 : c;
+        load64t<AL16>(P + 64 * cn, nxt);
+        mac.update(cur);
+    }
+}
+
 template <int MAC, bool SSL3>
 __global__ void __launch_bounds__(256) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
                                                  const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
@@ -119,15 +150,8 @@ __global__ void __launch_bounds__(256) mac_kernel(const tlsgpu_record* __restric
     M mac;
     mac.begin(st, mt.seq, R.content_type, n);
     const uint32_t nfull = (debug_skip & 2) ? 0u : (n >> 6);
-    uint32_t nxt[16];
-    if (nfull) load64(P, nxt);
-    for (uint32_t c = 0; c < nfull; c++) {
-        uint32_t cur[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) cur[j] = nxt[j];
-        if (c + 1 < nfull) load64(P + 64 * (c + 1), nxt);
-        mac.update(cur);
-    }
+    if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, P, nfull);
+    else mac_bulk<false>(mac, P, nfull);
     const uint32_t nf = n >> 6, r64 = n & 63;
     uint32_t tail[16];
     load_partial(P + 64 * nf, r64, tail);

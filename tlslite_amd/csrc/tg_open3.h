@@ -21,7 +21,7 @@
 //
 // Workspace per record: one 48-byte OpenMeta.
 #pragma once
-#include "tg_aesq.h"
+#include "tg_aes3.h"
 
 namespace tg {
 
@@ -250,15 +250,8 @@ __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record*
     M mac;
     mac.begin(st, mt.seq, R.content_type, n);
     const uint32_t nfull = n >> 6;
-    uint32_t nxt[16];
-    if (nfull) load64(P, nxt);
-    for (uint32_t c = 0; c < nfull; c++) {
-        uint32_t cur[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) cur[j] = nxt[j];
-        if (c + 1 < nfull) load64(P + 64 * (c + 1), nxt);
-        mac.update(cur);
-    }
+    if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, P, nfull);
+    else mac_bulk<false>(mac, P, nfull);
     uint32_t tail[16];
     load_partial(P + 64 * nfull, n & 63, tail);
     uint32_t m[8];
