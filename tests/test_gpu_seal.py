@@ -165,19 +165,29 @@ def test_pipeline_equals_sequential(kind):
     wl.free()
 
 
-@pytest.mark.parametrize("ilp", ["cbc1", "cbc2", "fused", "lane"])
+# AES seal kernel selections (environment switches read per launch by libtlsgpu)
+AES_IMPLS = {
+    "cbc1": {},                                   # default: cbc_kernel, column-word I/O, per-lane MAC loads
+    "cbc1io16": {"TLSGPU_CBC_IO": "16"},          # cbc_kernel<NR, IO16>: 16-byte I/O + quad transposes
+    "macquad": {"TLSGPU_MAC_LOAD": "quad"},       # mac_kernel<.., QL>: quad-cooperative loads
+    "cbc2": {"TLSGPU_CBC_ILP": "2"},              # cbc2_kernel: two chains per quad
+    "fused": {"TLSGPU_SEAL_IMPL": "fused"},       # single fused quad kernel
+    "lane": {"TLSGPU_SEAL_IMPL": "lane"},         # one lane per chain
+}
+
+
+@pytest.mark.parametrize("ilp", list(AES_IMPLS))
 @pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 1)), ("AES256-SHA256", (3, 3)), ("AES128-SHA", (3, 0))])
 def test_cbc_variants_chained_vs_oracle(ilp, suite, version, monkeypatch):
-    """Every AES seal kernel -- split path with cbc_kernel (one chain per quad) or
+    """Every AES seal kernel -- split path with cbc_kernel (one chain per quad;
+    column-word or 16-byte I/O; per-lane or quad-cooperative MAC loads) or
     cbc2_kernel (two chains per quad, bulk interleaved, IV/tail blocks one chain
     at a time), the fused single-kernel path, the 1-lane kernel -- on chains of
     mixed record counts and lengths (incl. empty and sub-block records) equals
     the oracle, including the final CBC residue and seqnum."""
     from oracle import oracle as O
-    if ilp.startswith("cbc"):
-        monkeypatch.setenv("TLSGPU_CBC_ILP", ilp[3])
-    else:
-        monkeypatch.setenv("TLSGPU_SEAL_IMPL", ilp)
+    for k, v in AES_IMPLS[ilp].items():
+        monkeypatch.setenv(k, v)
     T = _T()
     rng = np.random.default_rng(zlib.crc32(repr(("ilp", suite, version)).encode()))
     cipher, kl, ivl, mac, ml = O.SUITES[suite]
@@ -195,3 +205,41 @@ def test_cbc_variants_chained_vs_oracle(ilp, suite, version, monkeypatch):
         assert w == ocs[ci].seal(p, ct, fl), (ilp, suite, version, len(p))
     for s, o in zip(states, ocs):
         assert s.seqnum == o.seqnum and s.iv == o.iv
+
+
+@pytest.mark.parametrize("impl", ["cbc1", "cbc1io16", "macquad"])
+@pytest.mark.parametrize("pt_shift,wire_shift", [(0, 0), (4, 4), (0, 4), (4, 0), (1, 0), (0, 1), (3, 7)])
+@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES128-SHA", (3, 1)), ("RC4-SHA", (3, 1))])
+def test_unaligned_arenas_vs_oracle(pt_shift, wire_shift, suite, version, impl, monkeypatch):
+    """Record arenas off the 16-byte grid: every record's plaintext at
+    pt_off % 16 == pt_shift and its body at (wire_off + 5) % 16 == wire_shift.
+    The kernels pick 16-byte, dword or byte paths per record (and the MAC its
+    per-lane loads when a quad is not 16-byte aligned); output equals the oracle.
+    Equal-length records in runs of 4 so quad-cooperative MAC loads are taken
+    whenever the alignment allows."""
+    from oracle import oracle as O
+    if suite.startswith("RC4") and impl != "cbc1":
+        pytest.skip("AES kernel selections only")
+    for k, v in AES_IMPLS[impl].items():
+        monkeypatch.setenv(k, v)
+    T = _T()
+    rng = np.random.default_rng(zlib.crc32(repr(("unal", pt_shift, wire_shift, suite, version)).encode()))
+    cipher, kl, ivl, mac, ml = O.SUITES[suite]
+    states, ocs, recs = [], [], []
+    for ci in range(64):
+        key, iv, mk, fiv = rng.bytes(kl), rng.bytes(ivl), rng.bytes(ml), rng.bytes(ivl) if ivl else None
+        seq = int(rng.integers(0, 2 ** 40))
+        states.append(T.ConnectionState.for_suite(suite, version, key, iv, mk, fiv, seq))
+        ocs.append(O.Conn.for_suite(suite, version, key, iv, mk, fiv, seq))
+    for blk in range(16):
+        n = int(rng.choice([1, 17, 64, 100, 1434, 4096, 5003, 16384]))
+        for ci in range(4 * blk, 4 * blk + 4):
+            recs.append((ci, rng.bytes(n), 23, 0))
+    for _ in range(40):
+        ci = int(rng.integers(0, 64))
+        recs.append((ci, rng.bytes(int(rng.integers(0, 3000))), 23, 0))
+    out = T.seal(states, recs, pt_shift=pt_shift, wire_shift=wire_shift)
+    for (ci, p, ct, fl), w in zip(recs, out):
+        assert w == ocs[ci].seal(p, ct, fl), (suite, version, len(p), pt_shift, wire_shift)
+    for s, o in zip(states, ocs):
+        assert s.seqnum == o.seqnum

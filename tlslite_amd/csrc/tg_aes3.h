@@ -95,6 +95,37 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
     if (ok) st->seqnum = seq;
 }
 
+// value of register v in lane L of the calling lane's quad
+template <int L>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {
+    return quad_dpp<L * 0x55>(v);
+}
+template <int K>
+__device__ __forceinline__ uint32_t sel4(const uint32_t x[4], uint32_t q) {  // x[(q + K) & 3]
+    const uint32_t i = (q + K) & 3u;
+    return i == 0 ? x[0] : i == 1 ? x[1] : i == 2 ? x[2] : x[3];
+}
+// quad_perm control: lane q reads lane (q + K) & 3
+template <int K>
+constexpr int quad_rot_ctrl() {
+    return ((0 + K) & 3) | (((1 + K) & 3) << 2) | (((2 + K) & 3) << 4) | (((3 + K) & 3) << 6);
+}
+// 4x4 transpose across a quad: on entry lane q holds row q in x[0..3], on exit lane q
+// holds column q (x[i] = entry row i, element q).  Step K: every lane offers its element
+// (q - K) & 3 and reads lane (q + K) & 3, which offered exactly element q.
+__device__ __forceinline__ void quad_transpose(uint32_t x[4], uint32_t q) {
+    const uint32_t u0 = sel4<0>(x, q);
+    const uint32_t u1 = quad_dpp<quad_rot_ctrl<1>()>(sel4<3>(x, q));
+    const uint32_t u2 = quad_dpp<quad_rot_ctrl<2>()>(sel4<2>(x, q));
+    const uint32_t u3 = quad_dpp<quad_rot_ctrl<3>()>(sel4<1>(x, q));
+    // u_K belongs at index (q + K) & 3
+    const uint32_t u[4] = {u0, u1, u2, u3};
+    x[0] = sel4<0>(u, (4u - q) & 3u);
+    x[1] = sel4<0>(u, (5u - q) & 3u);
+    x[2] = sel4<0>(u, (6u - q) & 3u);
+    x[3] = sel4<0>(u, (7u - q) & 3u);
+}
+
 // 64-byte chunk load: 4 x dwordx4 when 16-byte aligned, else the generic path
 template <bool AL16>
 __device__ __forceinline__ void load64t(const uint8_t* p, uint32_t d[16]) {
@@ -126,7 +157,55 @@ __device__ __forceinline__ void mac_bulk(M& mac, const uint8_t* P, uint32_t nful
     }
 }
 
-template <int MAC, bool SSL3>
+// MAC over nfull 64-byte chunks of the quad's four records (equal nfull, 16-byte aligned
+// plaintext), loaded cooperatively: per load instruction lane q fetches bytes [16q, 16q+16)
+// of record L's chunk, so a quad reads a record's 64 contiguous bytes with one instruction
+// (a wave: 16 records x 64 B) instead of 64 scattered 16-byte pieces, which is what let the
+// MAC phase's plaintext stream slow the concurrent CBC phase.  Four quad transposes per
+// chunk hand every lane its own record's 16 words.
+template <class M>
+__device__ __forceinline__ void mac_bulk_quad(M& mac, const uint8_t* P, uint32_t nfull, uint32_t q) {
+    if (nfull == 0) return;
+    const uint32_t lo = (uint32_t)(uintptr_t)P, hi = (uint32_t)((uintptr_t)P >> 32);
+    const uint8_t* PL[4];
+    PL[0] = (const uint8_t*)(((uint64_t)quad_bcast<0>(hi) << 32) | quad_bcast<0>(lo)) + 16 * q;
+    PL[1] = (const uint8_t*)(((uint64_t)quad_bcast<1>(hi) << 32) | quad_bcast<1>(lo)) + 16 * q;
+    PL[2] = (const uint8_t*)(((uint64_t)quad_bcast<2>(hi) << 32) | quad_bcast<2>(lo)) + 16 * q;
+    PL[3] = (const uint8_t*)(((uint64_t)quad_bcast<3>(hi) << 32) | quad_bcast<3>(lo)) + 16 * q;
+    uint4 nxt[4];
+#pragma unroll
+    for (int L = 0; L < 4; L++) nxt[L] = *(const uint4*)PL[L];
+    for (uint32_t c = 0; c < nfull; c++) {
+        uint4 cur[4];
+#pragma unroll
+        for (int L = 0; L < 4; L++) cur[L] = nxt[L];
+        const uint32_t cn = c + 1 < nfull ? c + 1 : c;
+#pragma unroll
+        for (int L = 0; L < 4; L++) nxt[L] = *(const uint4*)(PL[L] + 64 * cn);
+        // lane q row L = record L bytes [16q, 16q+16); after the transpose lane q holds
+        // record q's sub-block s (x[s]) of component j: its word 4s + j
+        uint32_t d[16];
+        uint32_t x[4];
+        x[0] = cur[0].x; x[1] = cur[1].x; x[2] = cur[2].x; x[3] = cur[3].x;
+        quad_transpose(x, q);
+        d[0] = x[0]; d[4] = x[1]; d[8] = x[2]; d[12] = x[3];
+        x[0] = cur[0].y; x[1] = cur[1].y; x[2] = cur[2].y; x[3] = cur[3].y;
+        quad_transpose(x, q);
+        d[1] = x[0]; d[5] = x[1]; d[9] = x[2]; d[13] = x[3];
+        x[0] = cur[0].z; x[1] = cur[1].z; x[2] = cur[2].z; x[3] = cur[3].z;
+        quad_transpose(x, q);
+        d[2] = x[0]; d[6] = x[1]; d[10] = x[2]; d[14] = x[3];
+        x[0] = cur[0].w; x[1] = cur[1].w; x[2] = cur[2].w; x[3] = cur[3].w;
+        quad_transpose(x, q);
+        d[3] = x[0]; d[7] = x[1]; d[11] = x[2]; d[15] = x[3];
+        mac.update(d);
+    }
+}
+
+// QL: quad-cooperative plaintext loads (mac_bulk_quad) where a quad allows them; a
+// separate instantiation so the default kernel keeps its small register footprint
+// (a MAC wave must fit beside four cbc_kernel waves on a SIMD: 4 x 96 + 128 <= 512 VGPRs)
+template <int MAC, bool SSL3, bool QL = false>
 __global__ void __launch_bounds__(256) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
                                                  const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
                                                  const ConnState* __restrict__ states, int32_t* __restrict__ wire_len,
@@ -135,23 +214,45 @@ __global__ void __launch_bounds__(256) mac_kernel(const tlsgpu_record* __restric
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrecords) return;
-    const RecMeta mt = meta[r];
-    if (mt.epoch != epoch || mt.status != 1) return;
+    // no early exit before the bulk: the lanes of a quad exchange loaded data (DPP)
+    RecMeta mt = {};
+    bool act = r < nrecords;
+    if (act) {
+        mt = meta[r];
+        act = mt.epoch == epoch && mt.status == 1;
+    }
     set_prio(prio_of(debug_skip, 6, 0));
-    const ConnState* st = states + mt.state;
-    const tlsgpu_record R = recs[r];
+    const ConnState* st = states;
+    tlsgpu_record R = {};
+    const uint8_t* P = pt;
+    M mac;
+    if (act) {
+        st = states + mt.state;
+        R = recs[r];
+        P = pt + R.pt_off;
+        mac.begin(st, mt.seq, R.content_type, R.pt_len);
+    }
     const uint32_t n = R.pt_len;
+    const uint32_t nfull = (!act || (debug_skip & 2)) ? 0u : (n >> 6);
+    const bool al16 = ((uintptr_t)P & 15) == 0;
+    // quad-cooperative loads when the quad's four records are all sealed, 16-byte aligned
+    // and of equal chunk count
+    bool quad = false;
+    if constexpr (QL) {
+        const uint32_t key = (act && al16) ? nfull : 0xffffffffu;
+        quad = key != 0xffffffffu && quad_bcast<0>(key) == key && quad_bcast<1>(key) == key &&
+               quad_bcast<2>(key) == key && quad_bcast<3>(key) == key;
+        if (quad) mac_bulk_quad(mac, P, nfull, threadIdx.x & 3u);
+    }
+    if (!quad && act) {
+        if (al16) mac_bulk<true>(mac, P, nfull);
+        else mac_bulk<false>(mac, P, nfull);
+    }
+    if (!act) return;
     const uint32_t E = st->explicit_iv ? 16u : 0u;
     const uint32_t cur0 = E + n + DL;
     const uint32_t body = cur0 + (16 - (cur0 & 15));
-    const uint8_t* P = pt + R.pt_off;
     uint8_t* W = wire + R.wire_off;
-    M mac;
-    mac.begin(st, mt.seq, R.content_type, n);
-    const uint32_t nfull = (debug_skip & 2) ? 0u : (n >> 6);
-    if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, P, nfull);
-    else mac_bulk<false>(mac, P, nfull);
     const uint32_t nf = n >> 6, r64 = n & 63;
     uint32_t tail[16];
     load_partial(P + 64 * nf, r64, tail);
@@ -218,14 +319,16 @@ __device__ __forceinline__ void st32t(uint8_t* p, uint32_t v) {
 // branches and the prefetch index is clamped to the last block (never out of the record),
 // so the compiler's vmcnt waits cover only the loads a block actually consumes -- a
 // conditional load per block made it wait for the whole prefetch (vmcnt(0)) every group.
-template <int NR, bool AL>
+// PROBE (timing experiments only): 1 = no plaintext loads, 2 = no ciphertext stores.
+template <int NR, bool AL, int PROBE = 0>
 __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t* k, uint32_t iv,
                                              const uint8_t* P, uint8_t* O, uint32_t nb) {
     if (nb == 0) return iv;
     const uint32_t last = nb - 1;
     uint32_t f[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) f[i] = ld32t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
+    for (int i = 0; i < 8; i++)
+        f[i] = PROBE == 1 ? (uint32_t)i : ld32t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
     uint32_t b0 = 0;
     for (; b0 + 8 <= nb; b0 += 8) {
         uint32_t c[8];
@@ -234,12 +337,12 @@ __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t*
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t b = b0 + 8 + i;
-            f[i] = ld32t<AL>(P + 16 * (b < last ? b : last));
+            f[i] = PROBE == 1 ? b ^ c[i] : ld32t<AL>(P + 16 * (b < last ? b : last));
         }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(c[i], iv, k[0], 0x96), k);
-            st32t<AL>(O + 16 * (b0 + i), iv);
+            if (PROBE != 2) st32t<AL>(O + 16 * (b0 + i), iv);
         }
     }
 #pragma unroll
@@ -252,7 +355,43 @@ __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t*
     return iv;
 }
 
-template <int NR>
+// CBC over ng groups of 4 blocks with 16-byte I/O: lane q loads and stores block 4g+q whole
+// (one dwordx4 per lane, 64 contiguous bytes per quad and instruction -- a quarter of the
+// VMEM instructions of the column-word path, and full 64-byte segments), and two quad
+// transposes per group convert between that and the column-per-lane AES state.  The
+// prefetch runs D groups ahead with the index clamped to the last group.  P, O: the
+// record's first full block, both 16-byte aligned.
+template <int NR, int D = 4>
+__device__ __forceinline__ uint32_t cbc_bulk16(const QuadAes& aes, const uint32_t* k, uint32_t iv,
+                                               const uint8_t* P, uint8_t* O, uint32_t ng, uint32_t q) {
+    if (ng == 0) return iv;
+    const uint32_t last = ng - 1;
+    const uint8_t* Pq = P + 16 * q;
+    uint8_t* Oq = O + 16 * q;
+    uint4 f[D];
+#pragma unroll
+    for (int i = 0; i < D; i++) f[i] = *(const uint4*)(Pq + 64 * ((uint32_t)i < last ? (uint32_t)i : last));
+    for (uint32_t g = 0; g < ng; g++) {
+        uint32_t x[4] = {f[0].x, f[0].y, f[0].z, f[0].w};
+#pragma unroll
+        for (int i = 0; i + 1 < D; i++) f[i] = f[i + 1];
+        const uint32_t gn = g + D < last ? g + D : last;
+        f[D - 1] = *(const uint4*)(Pq + 64 * gn);
+        quad_transpose(x, q);  // lane q: column q of blocks 4g .. 4g+3
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(x[i], iv, k[0], 0x96), k);
+            x[i] = iv;
+        }
+        quad_transpose(x, q);  // lane q: block 4g+q
+        *(uint4*)(Oq + 64 * g) = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    return iv;
+}
+
+// IO16: 16-byte plaintext/ciphertext I/O (cbc_bulk16) for 16-byte aligned records; a
+// separate instantiation (it needs ~95 VGPRs against ~44, see mac_kernel)
+template <int NR, bool IO16 = false>
 __global__ void __launch_bounds__(C3_THREADS, 1)
 cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
            uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
@@ -294,7 +433,17 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
         }
         uint8_t* O = B + E + 4 * q;
         const uint32_t nb = (debug_skip & 1) ? 0u : (n >> 4);
-        iv = al ? cbc_bulk<NR, true>(aes, k, iv, P, O, nb) : cbc_bulk<NR, false>(aes, k, iv, P, O, nb);
+        if (debug_skip & 0x1000u)  // timing probe: bulk without plaintext loads (wrong ciphertext)
+            iv = cbc_bulk<NR, true, 1>(aes, k, iv, P, O, nb);
+        else if (debug_skip & 0x2000u)  // timing probe: bulk without ciphertext stores
+            iv = cbc_bulk<NR, true, 2>(aes, k, iv, P, O, nb);
+        else if (IO16 && ((((uintptr_t)(pt + R.pt_off)) | (uintptr_t)(B + E)) & 15) == 0) {
+            // 16-byte I/O for the 4-block groups, column words for the last nb % 4 blocks
+            const uint32_t ng = nb >> 2;
+            iv = cbc_bulk16<NR>(aes, k, iv, pt + R.pt_off, B + E, ng, q);
+            iv = cbc_bulk<NR, true>(aes, k, iv, P + 64 * ng, O + 64 * ng, nb & 3);
+        } else
+            iv = al ? cbc_bulk<NR, true>(aes, k, iv, P, O, nb) : cbc_bulk<NR, false>(aes, k, iv, P, O, nb);
         // tail blocks from the MAC kernel's slot
         const uint32_t r16 = n & 15;
         const uint8_t* slot = tails + (size_t)r * TAIL_SLOT + 4 * q;

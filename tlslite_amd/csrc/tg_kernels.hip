@@ -471,11 +471,19 @@ static int aes_impl() {  // TLSGPU_SEAL_IMPL, read per launch: split (default) /
 }
 static uint32_t debug_skip_flags() {
     static uint32_t skip = 0xffffffffu;
-    if (skip == 0xffffffffu) {  // TLSGPU_DEBUG_SKIP: 1 = no CBC bulk, 2 = no MAC bulk, bits 4-7 wave priorities (tg_aes3.h); timing experiments only
+    if (skip == 0xffffffffu) {  // TLSGPU_DEBUG_SKIP: 1 = no CBC bulk, 2 = no MAC bulk, bits 4-7 wave priorities, bits 12-13 CBC probes (tg_aes3.h); timing experiments only
         const char* e = getenv("TLSGPU_DEBUG_SKIP");
         skip = e ? (uint32_t)atoi(e) : 0u;
     }
     return skip;
+}
+// A/B switches for the seal kernels' memory paths, read per launch (tests flip them):
+// TLSGPU_MAC_LOAD=quad -> mac_kernel<.., QL> (quad-cooperative loads), TLSGPU_CBC_IO=16 ->
+// cbc_kernel<NR, IO16> (16-byte I/O).  Defaults (measured faster on cfg2):
+// per-lane MAC loads, column-word CBC I/O.
+static bool env_is(const char* name, char c0) {
+    const char* e = getenv(name);
+    return e && e[0] == c0;
 }
 static int cu_count() {
     static int ncu = 0;
@@ -502,8 +510,9 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((prefix_kernel<CID, MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains,
                        recs, states, wire_len, meta, nrecords, epoch);
-    hipLaunchKernelGGL((mac_kernel<MAC, SSL3>), dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords, pt, wire,
-                       states, wire_len, meta, tails, epoch, debug_skip_flags());
+    auto mk = env_is("TLSGPU_MAC_LOAD", 'q') ? mac_kernel<MAC, SSL3, true> : mac_kernel<MAC, SSL3, false>;
+    hipLaunchKernelGGL(mk, dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords, pt, wire, states, wire_len,
+                       meta, tails, epoch, debug_skip_flags());
     return hipGetLastError();
 }
 
@@ -532,12 +541,13 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
                            recs, nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
         return hipGetLastError();
     }
-    auto kern = cbc_kernel<NR>;
-    static bool attr = false;
-    if (!attr) {
+    const bool io16 = env_is("TLSGPU_CBC_IO", '1');
+    auto kern = io16 ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
+    static bool attr[2] = {false, false};
+    if (!attr[io16]) {
         hipError_t e = set_lds(kern, AES_LDS_BYTES);
         if (e != hipSuccess) return e;
-        attr = true;
+        attr[io16] = true;
     }
     hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C3_THREADS), AES_LDS_BYTES, s, chains, nchains, recs,
                        nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());

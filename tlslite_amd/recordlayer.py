@@ -160,13 +160,16 @@ class SealPipeline:
         self.close()
 
 
-def seal(states, records, stream=None):
+def seal(states, records, stream=None, pt_shift=0, wire_shift=0):
     """Seal records on the GPU.
 
     states:  list of ConnectionState (updated in place: seqnum, CBC residue, RC4)
     records: list of (state_index, payload, content_type=23, flags=0); records
              of one state are sealed in list order, like successive _sendMsg calls.
     Returns the list of wire records (b"" for an empty payload).
+    pt_shift / wire_shift (tests): place every record's plaintext at
+    pt_off % 16 == pt_shift and its body at (wire_off + 5) % 16 == wire_shift
+    instead of the 16-byte grid, to exercise the kernels' unaligned paths.
     """
     norm = []
     for r in records:
@@ -196,11 +199,13 @@ def seal(states, records, stream=None):
     pt_off = np.zeros(nrec, dtype=np.uint64)
     pos = 0
     for k, i in enumerate(order):
-        pt_off[k] = pos
+        pt_off[k] = pos + pt_shift
         pos += len(norm[i][1])
         pos += (-pos) % PT_ALIGN
-    pt_total = max(pos, 16)
+    pt_total = max(pos, 16) + pt_shift
     wire_off, wire_total = wire_offsets(wlen)
+    wire_off += np.uint64(wire_shift)
+    wire_total += wire_shift
     pt_host = np.zeros(pt_total, dtype=np.uint8)
     for k, i in enumerate(order):
         b = norm[i][1]

@@ -1,0 +1,343 @@
+// aes_layout_microbench.hip -- AES chains at a fixed number of chains per CU
+// (cfg2: 65,536 independent CBC chains on 256 CUs = 256 per CU), comparing lane
+// layouts of the LDS T-table round with no global-memory traffic in the loop:
+//   quad1   4 lanes/chain, column per lane, XOR tree dpp2(t2^dpp1(t3)) (tg_aesq.h), 16 waves/CU
+//   quad1b  4 lanes/chain, XOR tree ordered for the last lookup: ((k ^ dpp2 t2) ^ dpp3 t3) ^ t0 ^ dpp1 t1
+//   quad2   4 lanes/chain, 2 chains per quad interleaved,                    8 waves/CU
+//   quad2b  as quad2 with the quad1b XOR order
+//   pair1   2 lanes/chain (2 columns per lane, 8 lookups, one DPP swap),     8 waves/CU
+//   pair2   2 lanes/chain, 2 chains per lane pair,                           4 waves/CU
+//   lane1   1 lane/chain (16 lookups per lane),                              4 waves/CU
+//   *@512   the same at 512 chains per CU (cfg3 has 4,096 per CU)
+// Every layout encrypts the same chains with the same round keys; the host checks
+// that all final states agree.  Reports ns and shader cycles (s_memtime) per round,
+// the LDS-array floor fraction (16 lookups x chains / 32 per cycle) and the
+// cfg2-equivalent time of 1,027 blocks per chain.  Diagnostic tool only.
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/aes_layout_microbench.hip -o tools/aes_layout_mb.bin
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../tlslite_amd/csrc/tg_aesq.h"
+#include "../tlslite_amd/csrc/tg_hash.h"
+
+using namespace tg;
+
+constexpr int NR = 10;
+
+__device__ __forceinline__ uint32_t pair_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
+}
+
+// quad round with the XOR tree ordered for the lookup issue order (T2, T3, T0, T1):
+// column q = k_q ^ T2(q+2) ^ T3(q+3) ^ T0(q) ^ T1(q+1); only one DPP XOR follows the
+// last lookup.  kq = round-key column q (not pre-rotated).
+struct QuadAesB : QuadAes {
+    __device__ __forceinline__ uint32_t round_b(uint32_t x, uint32_t kq) const {
+        const uint32_t t2 = look<2, 2>(x);
+        const uint32_t t3 = look<3, 3>(x);
+        const uint32_t t0 = look<0, 0>(x);
+        const uint32_t t1 = look<1, 1>(x);
+        const uint32_t a = kq ^ quad_dpp<0x4E>(t2);
+        const uint32_t w = a ^ quad_dpp<0x93>(t3);
+        const uint32_t y = t0 ^ w;
+        return y ^ quad_dpp<0x39>(t1);
+    }
+    __device__ __forceinline__ uint32_t last_b(uint32_t x, uint32_t kq) const {
+        const uint32_t s2 = look<0, 2>(x) & 0xff0000u;
+        const uint32_t s3 = look<1, 3>(x) & 0xff000000u;
+        const uint32_t s0 = look<2, 0>(x) & 0xffu;
+        const uint32_t s1 = look<3, 1>(x) & 0xff00u;
+        const uint32_t a = kq ^ quad_dpp<0x4E>(s2);
+        const uint32_t w = a ^ quad_dpp<0x93>(s3);
+        return (s0 ^ w) ^ quad_dpp<0x39>(s1);
+    }
+};
+
+// 2 lanes per chain: lane h holds columns a = 2h, b = 2h+1.  Column j of the next
+// state = T0[b0(s_j)] ^ T1[b1(s_j+1)] ^ T2[b2(s_j+2)] ^ T3[b3(s_j+3)] ^ k_j; each lane
+// XORs the two terms of its own columns and, with the partner's key column folded
+// in, the two terms the partner needs; one DPP swap per column joins them.
+struct PairAes : QuadAes {
+    __device__ __forceinline__ void round(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
+        const uint32_t a2 = look<2, 2>(a), b3 = look<3, 3>(b), a1 = look<1, 1>(a), b2 = look<2, 2>(b);
+        const uint32_t a0 = look<0, 0>(a), b1 = look<1, 1>(b), b0 = look<0, 0>(b), a3 = look<3, 3>(a);
+        const uint32_t sA = __builtin_amdgcn_bitop3_b32(a2, b3, ka, 0x96);
+        const uint32_t sB = __builtin_amdgcn_bitop3_b32(a1, b2, kb, 0x96);
+        a = (a0 ^ b1) ^ pair_dpp(sA);
+        b = (b0 ^ a3) ^ pair_dpp(sB);
+    }
+    // final round: S-box byte B of s sits at byte B of table (B+2)&3
+    __device__ __forceinline__ void last(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
+        const uint32_t ta0 = look<2, 0>(a), tb1 = look<3, 1>(b), ta2 = look<0, 2>(a), tb3 = look<1, 3>(b);
+        const uint32_t tb0 = look<2, 0>(b), ta3 = look<1, 3>(a), ta1 = look<3, 1>(a), tb2 = look<0, 2>(b);
+        const uint32_t oA = perm(tb1, ta0, 0x0c0c0500u);
+        const uint32_t sA = perm(tb3, ta2, 0x07020c0cu) ^ ka;
+        const uint32_t oB = perm(ta3, tb0, 0x070c0c00u);
+        const uint32_t sB = perm(tb2, ta1, 0x0c06010cu) ^ kb;
+        a = oA ^ pair_dpp(sA);
+        b = oB ^ pair_dpp(sB);
+    }
+};
+
+__device__ __forceinline__ void lane_round(const QuadAes& L, uint32_t s[4], const uint32_t* k) {
+    uint32_t t[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        t[j] = L.look<0, 0>(s[j]) ^ L.look<1, 1>(s[(j + 1) & 3]) ^ L.look<2, 2>(s[(j + 2) & 3]) ^
+               L.look<3, 3>(s[(j + 3) & 3]) ^ k[j];
+#pragma unroll
+    for (int j = 0; j < 4; j++) s[j] = t[j];
+}
+__device__ __forceinline__ void lane_last(const QuadAes& L, uint32_t s[4], const uint32_t* k) {
+    uint32_t t[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        t[j] = ((L.look<2, 0>(s[j]) & 0xffu) | (L.look<3, 1>(s[(j + 1) & 3]) & 0xff00u) |
+                (L.look<0, 2>(s[(j + 2) & 3]) & 0xff0000u) | (L.look<1, 3>(s[(j + 3) & 3]) & 0xff000000u)) ^ k[j];
+#pragma unroll
+    for (int j = 0; j < 4; j++) s[j] = t[j];
+}
+
+__device__ __forceinline__ uint32_t init_word(uint32_t chain, uint32_t col) {
+    return (chain * 2654435761u) ^ (col * 0x9e3779b9u) ^ 0x5bd1e995u;
+}
+
+// LAYOUT: 4 = quad, 5 = quad with round_b, 2 = pair, 1 = lane.  CPC = chains per CU.
+// out[chain*4 + col] = final state; cyc[block] = s_memtime delta of wave 0
+template <int LAYOUT, int ILP, int CPC>
+__global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict__ ek, uint32_t* __restrict__ out,
+                                                     uint64_t* __restrict__ cyc, int blocks) {
+    aes_lds_fill(nullptr, false);
+    __syncthreads();
+    __builtin_amdgcn_s_setprio(1);  // as cbc_kernel: win issue arbitration over the MAC waves
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if constexpr (LAYOUT == 4 || LAYOUT == 5) {  // quad: lane q = column q
+        QuadAesB L;
+        L.init();
+        const uint32_t q = lane & 3;
+        const uint32_t quad = wave * 16 + (lane >> 2);
+        uint32_t k[NR + 1];
+        if constexpr (LAYOUT == 4) {
+            QuadAes::round_keys<NR>(ek, q, k);
+        } else {
+#pragma unroll
+            for (int r = 0; r <= NR; r++) k[r] = ek[4 * r + q];
+        }
+        uint32_t x[ILP];
+        uint32_t ch[ILP];
+#pragma unroll
+        for (int i = 0; i < ILP; i++) {
+            ch[i] = blockIdx.x * CPC + quad * ILP + i;
+            x[i] = init_word(ch[i], q);
+        }
+        for (int b = 0; b < blocks; b++) {
+#pragma unroll
+            for (int i = 0; i < ILP; i++) x[i] ^= k[0];
+#pragma unroll
+            for (int r = 1; r < NR; r++) {
+                uint32_t y[ILP];
+#pragma unroll
+                for (int i = 0; i < ILP; i++) y[i] = LAYOUT == 4 ? L.round<0>(x[i], k[r]) : L.round_b(x[i], k[r]);
+#pragma unroll
+                for (int i = 0; i < ILP; i++) x[i] = y[i];
+            }
+            uint32_t y[ILP];
+#pragma unroll
+            for (int i = 0; i < ILP; i++) y[i] = LAYOUT == 4 ? L.last(x[i], k[NR]) : L.last_b(x[i], k[NR]);
+#pragma unroll
+            for (int i = 0; i < ILP; i++) x[i] = y[i];
+        }
+#pragma unroll
+        for (int i = 0; i < ILP; i++) out[ch[i] * 4 + q] = x[i];
+    } else if constexpr (LAYOUT == 2) {  // pair: lane h = columns 2h, 2h+1
+        PairAes P;
+        P.init();
+        const uint32_t h = lane & 1;
+        const uint32_t pr = wave * 32 + (lane >> 1);
+        const uint32_t ca = 2 * h, pa = 2 * (1 - h);
+        const uint32_t kwa = ek[ca], kwb = ek[ca + 1];
+        uint32_t ka[NR + 1], kb[NR + 1];
+#pragma unroll
+        for (int r = 1; r <= NR; r++) {
+            ka[r] = ek[4 * r + pa];
+            kb[r] = ek[4 * r + pa + 1];
+        }
+        uint32_t a[ILP], bb[ILP], ch[ILP];
+#pragma unroll
+        for (int i = 0; i < ILP; i++) {
+            ch[i] = blockIdx.x * CPC + pr * ILP + i;
+            a[i] = init_word(ch[i], ca);
+            bb[i] = init_word(ch[i], ca + 1);
+        }
+        for (int b = 0; b < blocks; b++) {
+#pragma unroll
+            for (int i = 0; i < ILP; i++) {
+                a[i] ^= kwa;
+                bb[i] ^= kwb;
+            }
+#pragma unroll
+            for (int r = 1; r < NR; r++) {
+#pragma unroll
+                for (int i = 0; i < ILP; i++) P.round(a[i], bb[i], ka[r], kb[r]);
+            }
+#pragma unroll
+            for (int i = 0; i < ILP; i++) P.last(a[i], bb[i], ka[NR], kb[NR]);
+        }
+#pragma unroll
+        for (int i = 0; i < ILP; i++) {
+            out[ch[i] * 4 + ca] = a[i];
+            out[ch[i] * 4 + ca + 1] = bb[i];
+        }
+    } else {  // lane: one chain per lane
+        QuadAes L;
+        L.init();
+        const uint32_t c = blockIdx.x * CPC + wave * 64 + lane;
+        uint32_t s[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) s[j] = init_word(c, j);
+        uint32_t k[4 * (NR + 1)];
+#pragma unroll
+        for (int j = 0; j < 4 * (NR + 1); j++) k[j] = ek[j];
+        for (int b = 0; b < blocks; b++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) s[j] ^= k[j];
+#pragma unroll
+            for (int r = 1; r < NR; r++) lane_round(L, s, k + 4 * r);
+            lane_last(L, s, k + 4 * NR);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) out[c * 4 + j] = s[j];
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        cyc[2 * blockIdx.x] = t1 - t0;
+        cyc[2 * blockIdx.x + 1] = rt1 - rt0;
+    }
+}
+
+// VALU co-runner shaped like mac_kernel: one lane per "record", SHA-1 compressions
+// on register data, one 256-thread block per CU (one wave per SIMD).
+__global__ void __launch_bounds__(256) sha_corun(uint32_t* out, int iters) {
+    uint32_t h[8] = {1, 2, 3, 4, 5, 0, 0, 0};
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = threadIdx.x * 31 + i;
+    __builtin_amdgcn_s_setprio(0);
+    for (int i = 0; i < iters; i++) {
+        Hash<TLSGPU_MAC_SHA1>::compress(h, w);
+        w[i & 15] ^= h[0];
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4];
+}
+
+struct Res {
+    const char* name;
+    int cpc;
+    float ms;
+    double cyc;
+    std::vector<uint32_t> out;
+};
+
+static hipStream_t g_side = nullptr;
+static uint32_t* g_side_out = nullptr;
+
+template <int LAYOUT, int ILP, int CPC>
+static Res run(const char* name, const uint32_t* d_ek, int cus, int blocks, int corun = 0) {
+    const int lanes_per_chain = LAYOUT >= 4 ? 4 : LAYOUT;
+    const int threads = CPC * lanes_per_chain / ILP;
+    auto kern = bench_kernel<LAYOUT, ILP, CPC>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              AES_LDS_BYTES);
+    uint32_t* d_out;
+    uint64_t* d_cyc;
+    (void)hipMalloc(&d_out, (size_t)cus * CPC * 16);
+    (void)hipMalloc(&d_cyc, cus * 16);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    hipLaunchKernelGGL(kern, dim3(cus), dim3(threads), AES_LDS_BYTES, 0, d_ek, d_out, d_cyc, 20);
+    (void)hipDeviceSynchronize();
+    if (corun) hipLaunchKernelGGL(sha_corun, dim3(cus), dim3(256), 0, g_side, g_side_out, corun);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(kern, dim3(cus), dim3(threads), AES_LDS_BYTES, 0, d_ek, d_out, d_cyc, blocks);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    Res r;
+    r.name = name;
+    r.cpc = CPC;
+    (void)hipEventElapsedTime(&r.ms, e0, e1);
+    (void)hipDeviceSynchronize();
+    std::vector<uint64_t> cyc(2 * cus);
+    (void)hipMemcpy(cyc.data(), d_cyc, cus * 16, hipMemcpyDeviceToHost);
+    double s = 0, rt = 0;
+    for (int i = 0; i < cus; i++) {
+        s += (double)cyc[2 * i];
+        rt += (double)cyc[2 * i + 1];
+    }
+    r.cyc = s / cus;
+    const double ghz = s / (rt * 10.0);  // s_memrealtime ticks at 100 MHz
+    r.out.resize((size_t)cus * CPC * 4);
+    (void)hipMemcpy(r.out.data(), d_out, r.out.size() * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_cyc);
+    const double rounds = (double)blocks * NR;
+    const double floor_cyc = CPC * 16.0 / 32.0;  // LDS-array cycles per round
+    const double ns = r.ms * 1e6 / rounds;
+    printf("%-7s chains/CU=%3d waves/CU=%2d%s  %7.2f ns/round  clock %.2f GHz  %5.1f G lookups/s/CU  "
+           "LDS-floor frac %.2f  cfg2-equiv %.3f ms\n",
+           name, CPC, threads / 64, corun ? " +sha" : "     ", ns, ghz, CPC * 16.0 / ns,
+           floor_cyc / (ns * ghz), r.ms * (256.0 / CPC) * 1027.0 / blocks);
+    fflush(stdout);
+    return r;
+}
+
+static int compare(const std::vector<Res>& rs) {
+    int bad = 0;
+    for (size_t i = 1; i < rs.size(); i++)
+        if (rs[i].out != rs[0].out) {
+            printf("MISMATCH: %s differs from %s\n", rs[i].name, rs[0].name);
+            bad = 1;
+        }
+    return bad;
+}
+
+int main(int argc, char** argv) {
+    const int blocks = argc > 1 ? atoi(argv[1]) : 1027;
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    printf("CUs %d, %d blocks per chain\n", cus, blocks);
+    uint32_t ek[4 * (NR + 1)];
+    for (int i = 0; i < 4 * (NR + 1); i++) ek[i] = 0x01234567u * (i + 3) ^ (i << 20);
+    uint32_t* d_ek;
+    (void)hipMalloc(&d_ek, sizeof(ek));
+    (void)hipMemcpy(d_ek, ek, sizeof(ek), hipMemcpyHostToDevice);
+    (void)hipStreamCreateWithFlags(&g_side, hipStreamNonBlocking);
+    (void)hipMalloc(&g_side_out, (size_t)cus * 256 * 4);
+    std::vector<Res> a;
+    a.push_back(run<4, 1, 256>("quad1", d_ek, cus, blocks));
+    a.push_back(run<5, 1, 256>("quad1b", d_ek, cus, blocks));
+    a.push_back(run<4, 2, 256>("quad2", d_ek, cus, blocks));
+    a.push_back(run<5, 2, 256>("quad2b", d_ek, cus, blocks));
+    a.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks));
+    a.push_back(run<2, 2, 256>("pair2", d_ek, cus, blocks));
+    a.push_back(run<1, 1, 256>("lane1", d_ek, cus, blocks));
+    std::vector<Res> b;
+    b.push_back(run<5, 2, 512>("quad2b", d_ek, cus, blocks));
+    b.push_back(run<4, 2, 512>("quad2", d_ek, cus, blocks));
+    b.push_back(run<2, 2, 512>("pair2", d_ek, cus, blocks));
+    b.push_back(run<2, 1, 512>("pair1", d_ek, cus, blocks));
+    b.push_back(run<1, 1, 512>("lane1", d_ek, cus, blocks));
+    // beside a mac_kernel-shaped VALU load (about 1.5x the AES kernel's duration)
+    std::vector<Res> c;
+    c.push_back(run<4, 1, 256>("quad1", d_ek, cus, blocks, 2 * blocks));
+    c.push_back(run<5, 1, 256>("quad1b", d_ek, cus, blocks, 2 * blocks));
+    c.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks, 2 * blocks));
+    c.push_back(run<4, 1, 256>("quad1", d_ek, cus, blocks, blocks / 3));
+    c.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks, blocks / 3));
+    const int bad = compare(a) | compare(b) | compare(c);
+    if (!bad) printf("all layouts agree\n");
+    return bad;
+}
