@@ -254,8 +254,20 @@ class Workload:
         var = self.launches[0][0]
         c, m = var & 0xff, (var >> 8) & 0xff
         if c in (N.CIPHER_AES128, N.CIPHER_AES256) and m in (N.MAC_SHA1, N.MAC_SHA256):
-            return "cbc_kernel<%d>" % (10 if c == N.CIPHER_AES128 else 14)
+            return "cbc_kernel<%d, false>" % (10 if c == N.CIPHER_AES128 else 14)
         return "seal_kernel"
+
+    def aes_lookups(self):
+        """LDS T-table lookups of one seal call when every launch is an AES suite:
+        16 per round per 16-byte block (4 state columns x 4 tables), NR rounds,
+        blocks = explicit IV + body of every sealed record = (wire_len - 5) / 16.
+        None for workloads with RC4 / 3DES launches."""
+        nr = {N.CIPHER_AES128: 10, N.CIPHER_AES256: 14}
+        if any((var & 0xff) not in nr for var, _, _ in self.launches):
+            return None
+        blocks = np.maximum(self.wire_len.astype(np.int64) - 5, 0) // 16
+        return int(16 * nr[self.launches[0][0] & 0xff] * int(blocks.sum())) if len(
+            {var & 0xff for var, _, _ in self.launches}) == 1 else None
 
     def free(self):
         for name in ("d_pt", "d_wire", "d_len", "d_recs", "d_states", "d_states0", "d_orecs", "d_opt", "d_ostatus",

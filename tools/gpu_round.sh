@@ -8,7 +8,7 @@ TAG=${1:-r01}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 120 python tools/dbg_open.py 4096 > $O/dbg_open.log 2>&1 || { echo "dbg_open failed"; cat $O/dbg_open.log; exit 1; }
 cat $O/dbg_open.log

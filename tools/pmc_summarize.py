@@ -1,11 +1,16 @@
 """Summarize tools/pmc_kernels.sh passes: per kernel (name stem), the median
 over full-size dispatches of every counter, the kernel's median duration,
-and the per-seal-call HBM traffic -> profiles/pmc_<cfg>.json.
+and its HBM traffic -> profiles/pmc_<cfg>.json.
 
 FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads 1/2 of the
 bytes of wide coalesced reads (MI355X_MICROARCH.md §HBM), so HBM bytes =
 (2*FETCH_SIZE + WRITE_SIZE)*1024, the raw sum recorded beside it.  SQ cycle
-counters (SQ_WAVE_CYCLES, SQ_WAIT_*, SQ_ACTIVE_*) count quad-cycles."""
+counters (SQ_WAVE_CYCLES, SQ_WAIT_*, SQ_ACTIVE_*) count quad-cycles.
+
+`hbm_bytes_per_launch` is the dominant kernel's traffic (the kernel whose
+roofline bench.py reports); `seal_call_hbm_bytes` sums the kernels of one seal
+call.  The bench's set-up kernels (synthetic plaintext fill, buffer zeroing)
+are listed but excluded from both."""
 import csv
 import glob
 import json
@@ -15,6 +20,8 @@ import statistics
 import sys
 
 out, cfg = sys.argv[1], sys.argv[2]
+SETUP = ("fill_kernel", "__amd_rocclr_fillBuffer")  # bench set-up / memsets, not the seal call
+DOMINANT = ("cbc_kernel", "cbc2_kernel", "seal_aesq_kernel", "seal_kernel")
 
 
 def stem(name):
@@ -22,6 +29,10 @@ def stem(name):
     if m:
         return m.group(1) + (m.group(2) or "")
     return name.split("(")[0][:60]
+
+
+def hbm_bytes(row):
+    return int((2 * row.get("FETCH_SIZE", 0) + row.get("WRITE_SIZE", 0)) * 1024)
 
 
 counters = {}   # stem -> counter -> {dispatch: value}
@@ -48,15 +59,21 @@ for k, cs in counters.items():
     if ds:
         top = max(ds)
         row["duration_ms"] = statistics.median([x for x in ds if x >= 0.3 * top]) / 1e6
+    if "FETCH_SIZE" in row or "WRITE_SIZE" in row:
+        row["hbm_bytes"] = hbm_bytes(row)
     res["kernels"][k] = row
-tf = sum(r.get("FETCH_SIZE", 0) for r in res["kernels"].values())
-tw = sum(r.get("WRITE_SIZE", 0) for r in res["kernels"].values())
-res["fetch_kib_raw"] = tf
-res["write_kib"] = tw
-res["hbm_bytes_per_launch_raw"] = int((tf + tw) * 1024)
-res["hbm_bytes_per_launch"] = int((2 * tf + tw) * 1024)
-res["note"] = ("per seal call (sum over its kernels); hbm_bytes_per_launch = (2*FETCH_SIZE + WRITE_SIZE)*1024 "
-               "(gfx950 FETCH_SIZE halves wide reads)")
+
+seal = {k: r for k, r in res["kernels"].items() if not k.startswith(SETUP)}
+dom = [k for k in seal if k.startswith(DOMINANT)]
+dom = max(dom, key=lambda k: seal[k].get("duration_ms", 0)) if dom else None
+res["dominant_kernel"] = dom
+res["hbm_bytes_per_launch"] = seal[dom].get("hbm_bytes") if dom else None
+res["hbm_bytes_per_launch_raw"] = (int((seal[dom].get("FETCH_SIZE", 0) + seal[dom].get("WRITE_SIZE", 0)) * 1024)
+                                   if dom else None)
+res["seal_call_hbm_bytes"] = sum(r.get("hbm_bytes", 0) for r in seal.values())
+res["note"] = ("hbm_bytes_per_launch: the dominant kernel's (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch "
+               "(gfx950 FETCH_SIZE halves wide reads); seal_call_hbm_bytes: sum over the seal call's kernels; "
+               "set-up kernels (%s) excluded" % ", ".join(SETUP))
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 with open(os.path.join(root, "profiles", "pmc_%s.json" % cfg), "w") as fh:
     json.dump(res, fh, indent=1)
