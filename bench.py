@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--records", type=int, default=None, help="override record count (debug)")
     ap.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline")
     ap.add_argument("--no-check", action="store_true", help="skip the full-batch parity check")
+    ap.add_argument("--no-derive", dest="derive", action="store_false",
+                    help="skip the batched key-derivation measurement")
     ap.add_argument("--no-open", dest="open", action="store_false", help="skip the open-path measurement")
     ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false",
                     help="skip the PCIe-inclusive measurement (profiling runs)")
@@ -196,6 +198,49 @@ def open_rate(wl, stream, steps):
                       "padding/seqnum pass, per-record MAC verify); median of HIP-event-timed calls"}
 
 
+def derive_rate(stream, nconn=4096, steps=10):
+    """Batched _calcPendingStates (tlsgpu_derive_states_dev) for cfg4's 4096
+    connections: master secret -> key block (TLS 1.2 PRF_1_2) -> pending
+    write/read states in HBM.  A sample of key blocks is checked against
+    the CPU oracle's PRF."""
+    import ctypes
+    from tlslite_amd import _native as N
+    from tlslite_amd.constants import SUITE_NAMES
+    from tlslite_amd.device import DeviceBuffer, Event
+    rng = np.random.default_rng(4)
+    descs = (N.DeriveDesc * nconn)()
+    raw = np.frombuffer(descs, dtype=np.uint8).reshape(nconn, ctypes.sizeof(N.DeriveDesc))
+    raw[:, :128] = rng.integers(0, 256, size=(nconn, 128), dtype=np.uint8)
+    for d in descs:
+        d.suite, d.ver_major, d.ver_minor, d.client = SUITE_NAMES["AES128-SHA"], 3, 3, 1
+    dd = DeviceBuffer(ctypes.sizeof(descs))
+    dd.upload(bytes(descs))
+    ws, rs = DeviceBuffer(nconn * N.CONN_STATE_BYTES), DeviceBuffer(nconn * N.CONN_STATE_BYTES)
+    kb, st = DeviceBuffer(nconn * N.KEY_BLOCK_MAX), DeviceBuffer(4 * nconn)
+    ms = []
+    for it in range(steps + 1):
+        a, b = Event(), Event()
+        a.record(stream)
+        N.call("tlsgpu_derive_states_dev", dd.ptr, nconn, ws.ptr, rs.ptr, None, kb.ptr, st.ptr, stream.handle)
+        b.record(stream)
+        stream.synchronize()
+        if it:
+            ms.append(a.elapsed_ms(b))
+    status = st.download().view(np.int32)
+    kbs = kb.download().reshape(nconn, N.KEY_BLOCK_MAX)
+    exact = bool((status == 0).all())
+    from oracle import oracle as O  # parity checker only
+    for i in rng.choice(nconn, 16, replace=False):
+        ref, _ = O.key_block((3, 3), "AES128-SHA", raw[i, :48].tobytes(), raw[i, 48:80].tobytes(),
+                             raw[i, 80:112].tobytes())
+        exact = exact and kbs[i, :len(ref)].tobytes() == ref
+    t = float(np.median(ms))
+    return {"connections": nconn, "ms": round(t, 4), "conns_per_s": round(nconn / (t / 1e3)),
+            "key_blocks_exact_sample": exact,
+            "method": "tlsgpu_derive_states_dev: TLS 1.2 PRF_1_2 key block + slicing + AES-128 key schedule + "
+                      "HMAC-SHA1 midstates, one lane per connection; median of HIP-event-timed calls"}
+
+
 def main():
     args = parse()
     from tlslite_amd.shard import ShardGroup
@@ -300,6 +345,13 @@ def main():
         except Exception as e:  # reported, never silently replaced
             open_res = {"error": str(e)}
 
+    derive_res = None
+    if D.world == 1 and args.derive:
+        try:
+            derive_res = derive_rate(stream)
+        except Exception as e:  # reported, never silently replaced
+            derive_res = {"error": str(e)}
+
     host_inc = None
     if D.world == 1 and args.host_inclusive:
         try:
@@ -335,6 +387,7 @@ def main():
             "bit_exact": bit_exact,
             "host_inclusive": host_inc,
             "open": open_res,
+            "derive": derive_res,
         }
         print(json.dumps(out))
     D.close()

@@ -19,6 +19,12 @@
  *                              utils/openssl_tripledes.py:29-47 (the stateful
  *                              cipher-object encrypt/decrypt behind
  *                              utils/cipherfactory.py:31-102)
+ *   tlsgpu_derive_states_dev . tlsrecordlayer.py:1061-1149 (_calcPendingStates:
+ *                              key block PRF :1097-1114, slicing :1117-1126,
+ *                              cipher/MAC objects :1127-1136, side :1138-1143)
+ *                              and mathtls.py:24-82 (P_hash, PRF, PRF_1_2,
+ *                              PRF_SSL, calcMasterSecret), batched over
+ *                              connections on the device
  *   tlsgpu_conn_state_get_* .. the state tlslite keeps in python objects:
  *                              Python_AES.IV (python_aes.py:44), Python_RC4.S/i/j
  *                              (python_rc4.py:21-23,36-37), _ConnectionState.seqnum
@@ -123,6 +129,23 @@ typedef struct tlsgpu_span {
     uint32_t state;
 } tlsgpu_span;
 
+/* One connection's post-handshake key material: the inputs of
+ * _calcPendingStates (tlsrecordlayer.py:1061) and, with
+ * TLSGPU_DERIVE_PREMASTER, of calcMasterSecret (mathtls.py:70). */
+#define TLSGPU_DERIVE_PREMASTER 1 /* secret is the 48-byte premaster secret */
+#define TLSGPU_KEY_BLOCK_MAX 160  /* 2 * (32 + 32 + 16): AES256-SHA256 */
+typedef struct tlsgpu_derive_desc {
+    uint8_t secret[48];        /* master secret (or premaster, see flags) */
+    uint8_t client_random[32];
+    uint8_t server_random[32];
+    uint8_t fixed_iv[16];      /* this side's fixedIVBlock (first IV-length bytes; TLS >= 1.1 block ciphers) */
+    uint16_t suite;            /* CipherSuite id (constants.py:159-201) */
+    uint8_t ver_major, ver_minor;
+    uint8_t client;            /* 1: this side is the client (self._client, tlsrecordlayer.py:1138) */
+    uint8_t flags;             /* TLSGPU_DERIVE_* */
+    uint8_t reserved[2];
+} tlsgpu_derive_desc;
+
 typedef struct tlsgpu_stream_s *tlsgpu_stream;
 typedef struct tlsgpu_event_s *tlsgpu_event;
 
@@ -225,6 +248,16 @@ int tlsgpu_cipher_dev(const tlsgpu_span *spans, uint32_t nspans, const uint8_t *
 
 /* ---- synthetic input (bench / tests): byte i = byte (i&7) of
  * splitmix64(seed + (i>>3)), little-endian, for i in [start, start+bytes). */
+/* Batched key derivation: for each descriptor, derive the key block and
+ * build this side's pending write and read states (device pointers,
+ * n states each), exactly as tlsgpu_conn_state_init would from the same
+ * slices (the read state gets an all-zero fixed IV, which only the sender
+ * uses).  master_out (48 B per connection) and key_block_out
+ * (TLSGPU_KEY_BLOCK_MAX B per connection, zero-padded) may be NULL.
+ * status[i] = 0, or TLSGPU_EINVAL for an unknown suite / bad version. */
+int tlsgpu_derive_states_dev(const tlsgpu_derive_desc *descs, uint32_t n, tlsgpu_conn_state *write_states,
+                             tlsgpu_conn_state *read_states, uint8_t *master_out, uint8_t *key_block_out,
+                             int32_t *status, tlsgpu_stream s);
 int tlsgpu_fill_pattern(uint8_t *dptr, size_t bytes, uint64_t seed, uint64_t start, tlsgpu_stream s);
 
 #ifdef __cplusplus

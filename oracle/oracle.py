@@ -57,6 +57,8 @@ def _load():
     lib.ora_cipher_decrypt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     lib.ora_hash.argtypes = [ctypes.c_int, u8p, ctypes.c_size_t, ctypes.c_void_p]
     lib.ora_hmac.argtypes = [ctypes.c_int, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, ctypes.c_void_p]
+    lib.ora_prf.argtypes = [ctypes.c_int, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, u8p, ctypes.c_size_t,
+                            ctypes.c_void_p, ctypes.c_size_t]
     lib.ora_conn_get_iv.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     lib.ora_conn_get_seq.argtypes = [ctypes.c_void_p]
     lib.ora_conn_get_seq.restype = ctypes.c_uint64
@@ -163,6 +165,34 @@ def hmac_(alg, key, data):
     out = ctypes.create_string_buffer(32)
     lib().ora_hmac(MAC[alg], bytes(key), len(key), bytes(data), len(data), out)
     return out.raw[: {"sha1": 20, "sha256": 32, "md5": 16}[alg]]
+
+
+def prf(version, secret, label, seed, length):
+    """PRF / PRF_1_2 / PRF_SSL by version (mathtls.py:37-68)."""
+    out = ctypes.create_string_buffer(max(1, length))
+    rc = lib().ora_prf(tuple(version)[1], bytes(secret), len(secret), bytes(label), len(label), bytes(seed),
+                       len(seed), out, length)
+    if rc:
+        raise ValueError("ora_prf: bad arguments")
+    return out.raw[:length]
+
+
+def master_secret(version, premaster, client_random, server_random):
+    """calcMasterSecret (mathtls.py:70-82)."""
+    return prf(version, premaster, b"master secret", bytes(client_random) + bytes(server_random), 48)
+
+
+def key_block(version, suite, master, client_random, server_random):
+    """_calcPendingStates key block (tlsrecordlayer.py:1097-1114) and its
+    slices in Parser order (:1117-1126)."""
+    _, kl, ivl, _, ml = SUITES[suite]
+    kb = prf(version, master, b"key expansion", bytes(server_random) + bytes(client_random), 2 * (ml + kl + ivl))
+    parts, pos = {}, 0
+    for name, size in (("client_mac", ml), ("server_mac", ml), ("client_key", kl), ("server_key", kl),
+                       ("client_iv", ivl), ("server_iv", ivl)):
+        parts[name] = kb[pos:pos + size]
+        pos += size
+    return kb, parts
 
 
 def fill_pattern(n, seed, start=0):

@@ -374,6 +374,59 @@ void ora_hmac(int alg, const uint8_t *key, size_t klen, const uint8_t *msg, size
     h_init(&c, alg); h_update(&c, op, 64); h_update(&c, inner, (size_t)hash_dlen(alg)); h_final(&c, out);
 }
 
+/* P_hash (mathtls.py:24-35): A(0) = seed, A(i) = HMAC(secret, A(i-1)),
+ * output HMAC(secret, A(i) || seed)...; XORed into out. */
+static void p_hash_xor(int alg, const uint8_t *secret, size_t slen, const uint8_t *seed, size_t seedlen,
+                       uint8_t *out, size_t length) {
+    uint8_t a[32], blk[32], msg[32 + 256];
+    size_t d = (size_t)hash_dlen(alg);
+    ora_hmac(alg, secret, slen, seed, seedlen, a);
+    for (size_t pos = 0; pos < length; pos += d) {
+        memcpy(msg, a, d);
+        memcpy(msg + d, seed, seedlen);
+        ora_hmac(alg, secret, slen, msg, d + seedlen, blk);
+        for (size_t i = 0; i < d && pos + i < length; i++) out[pos + i] ^= blk[i];
+        ora_hmac(alg, secret, slen, a, d, a);
+    }
+}
+
+/* PRF by protocol version: (3,0) PRF_SSL (mathtls.py:55-68; label unused),
+ * (3,1)/(3,2) PRF = P_MD5(S1) ^ P_SHA1(S2) with S1/S2 the ceil/floor halves
+ * (mathtls.py:37-50), (3,3) PRF_1_2 = P_SHA256 (mathtls.py:52-53).
+ * label + seed <= 256 bytes. */
+int ora_prf(int vmin, const uint8_t *secret, size_t slen, const uint8_t *label, size_t llen,
+            const uint8_t *seed, size_t seedlen, uint8_t *out, size_t length) {
+    uint8_t ls[256];
+    if (llen + seedlen > sizeof ls || vmin < 0 || vmin > 3) return -1;
+    memset(out, 0, length);
+    if (vmin == 0) {
+        uint8_t msg[26 + 64 + 256], inner[20], blk[16];
+        if (26 + slen + seedlen > sizeof msg || length > 26 * 16) return -1;
+        for (size_t x = 0, pos = 0; pos < length; x++, pos += 16) {
+            size_t m = 0;
+            for (size_t r = 0; r <= x; r++) msg[m++] = (uint8_t)('A' + x);
+            memcpy(msg + m, secret, slen); m += slen;
+            memcpy(msg + m, seed, seedlen); m += seedlen;
+            ora_hash(ORA_MAC_SHA1, msg, m, inner);
+            memcpy(msg, secret, slen);
+            memcpy(msg + slen, inner, 20);
+            ora_hash(ORA_MAC_MD5, msg, slen + 20, blk);
+            for (size_t i = 0; i < 16 && pos + i < length; i++) out[pos + i] = blk[i];
+        }
+        return 0;
+    }
+    memcpy(ls, label, llen);
+    memcpy(ls + llen, seed, seedlen);
+    if (vmin == 3) {
+        p_hash_xor(ORA_MAC_SHA256, secret, slen, ls, llen + seedlen, out, length);
+    } else {
+        size_t h1 = (slen + 1) / 2, h2 = slen / 2;
+        p_hash_xor(ORA_MAC_MD5, secret, h1, ls, llen + seedlen, out, length);
+        p_hash_xor(ORA_MAC_SHA1, secret + h2, slen - h2, ls, llen + seedlen, out, length);
+    }
+    return 0;
+}
+
 /* record MAC over seq||type||[ver]||len16||P: tlsrecordlayer.py:568-584,
  * SSL3 variant via MAC_SSL (mathtls.py:125-151): pad repeated 40 (SHA) / 48 (MD5) */
 static void record_mac(const ora_conn *c, uint64_t seq, int ctype, const uint8_t *p, size_t n, uint8_t *out) {

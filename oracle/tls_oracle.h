@@ -35,6 +35,8 @@ int ora_cipher_encrypt(ora_conn *c, uint8_t *b, size_t n);
 int ora_cipher_decrypt(ora_conn *c, uint8_t *b, size_t n);
 void ora_hash(int alg, const uint8_t *p, size_t n, uint8_t *out);
 void ora_hmac(int alg, const uint8_t *key, size_t klen, const uint8_t *msg, size_t n, uint8_t *out);
+int ora_prf(int vmin, const uint8_t *secret, size_t slen, const uint8_t *label, size_t llen,
+            const uint8_t *seed, size_t seedlen, uint8_t *out, size_t length);
 void ora_conn_get_iv(const ora_conn *c, uint8_t *iv16);
 uint64_t ora_conn_get_seq(const ora_conn *c);
 void ora_conn_get_rc4(const ora_conn *c, uint8_t *S256, int *i, int *j);

@@ -181,3 +181,22 @@ def test_golden_open_chains(golden):
         _check_final(c, case)
         n += 1
     assert n == 22
+
+
+def test_prf_golden_key_derivations(golden):
+    """oracle PRF / PRF_1_2 / PRF_SSL (mathtls.py:24-82) against the 21
+    calcMasterSecret + _calcPendingStates derivations captured from the
+    reference (all four protocol versions)."""
+    n, versions = 0, set()
+    for c in golden:
+        if c["kind"] != "keys":
+            continue
+        v = tuple(c["version"])
+        cr, sr = bytes.fromhex(c["client_random"]), bytes.fromhex(c["server_random"])
+        ms = O.master_secret(v, bytes.fromhex(c["premaster"]), cr, sr)
+        assert ms.hex() == c["master"], c["name"]
+        kb, _ = O.key_block(v, c["suite"], ms, cr, sr)
+        assert kb.hex() == c["key_block"], c["name"]
+        n += 1
+        versions.add(v)
+    assert n >= 15 and versions == {(3, 0), (3, 1), (3, 2), (3, 3)}

@@ -41,6 +41,16 @@ class Span(ctypes.Structure):  # tlsgpu_span
     _fields_ = [("off", ctypes.c_uint64), ("len", ctypes.c_uint32), ("state", ctypes.c_uint32)]
 
 
+class DeriveDesc(ctypes.Structure):  # tlsgpu_derive_desc
+    _fields_ = [("secret", ctypes.c_uint8 * 48), ("client_random", ctypes.c_uint8 * 32),
+                ("server_random", ctypes.c_uint8 * 32), ("fixed_iv", ctypes.c_uint8 * 16),
+                ("suite", ctypes.c_uint16), ("ver_major", ctypes.c_uint8), ("ver_minor", ctypes.c_uint8),
+                ("client", ctypes.c_uint8), ("flags", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 2)]
+
+
+DERIVE_PREMASTER = 1
+KEY_BLOCK_MAX = 160
+assert ctypes.sizeof(DeriveDesc) == 136
 assert ctypes.sizeof(Record) == 24 and ctypes.sizeof(Chain) == 16
 assert ctypes.sizeof(OpenRecord) == 24 and ctypes.sizeof(Span) == 16
 
@@ -88,6 +98,7 @@ SIGNATURES = [
     ("tlsgpu_open_workspace_bytes", _sz, [_u32]),
     ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
     ("tlsgpu_cipher_dev", _i, [_vp, _u32, _vp, _vp, _vp, _i, _i, _vp]),
+    ("tlsgpu_derive_states_dev", _i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("tlsgpu_fill_pattern", _i, [_vp, _sz, _u64, _u64, _vp]),
 ]
 

@@ -5,7 +5,8 @@
     (calcMasterSecret, tlslite/mathtls.py:70-82) with the TLS 1.0/1.1 PRF,
     the TLS 1.2 PRF_1_2 and SSL 3.0 PRF_SSL (mathtls.py:24-68).  This is
     per-connection control plane on the host (stdlib hmac/hashlib), not the
-    hot path.
+    hot path; `derive_pending_states_gpu` does the same for thousands of
+    connections in one launch (tg_derive.h) and leaves the states in HBM.
   * `RecordLayer`: write()/read() over a socket with every record sealed and
     opened by the gfx950 kernels -- the shape of TLSRecordLayer.write/read
     (tlsrecordlayer.py:163-255) once the handshake is done.
@@ -13,12 +14,15 @@
 The handshake itself (RSA/SRP/DH, certificates, Finished) is out of scope:
 see DESIGN.md.
 """
+import ctypes
 import hashlib
 import hmac
 import os
 
+import numpy as np
+
 from . import _native as N
-from .constants import ContentType, suite_primitives
+from .constants import SUITE_NAMES, ContentType, suite_primitives
 from .recordlayer import BadRecordMAC, DecryptionFailed, open_records, parse_records, plan_write, seal
 from .state import ConnectionState
 
@@ -96,6 +100,68 @@ def pending_states(version, suite, master, client_random, server_random, client,
     r = ConnectionState(cipher, mac, version, kp[peer + "_key"], kp[peer + "_iv"], kp[peer + "_mac"],
                         bytes(ivl) if need_fiv else None)
     return w, r
+
+
+class DerivedStates:
+    """Result of `derive_pending_states_gpu`: this side's pending write and
+    read states of n connections, resident in HBM (n * 2048 B each) where
+    the seal/open kernels take them, plus per-connection status."""
+
+    def __init__(self, n, write, read, master, key_block, status):
+        self.n, self.write, self.read = n, write, read
+        self.master, self.key_block, self.status = master, key_block, status
+
+    def write_state_bytes(self, i):
+        return bytes(self.write.download(N.CONN_STATE_BYTES, i * N.CONN_STATE_BYTES))
+
+    def read_state_bytes(self, i):
+        return bytes(self.read.download(N.CONN_STATE_BYTES, i * N.CONN_STATE_BYTES))
+
+
+def derive_pending_states_gpu(conns, premaster=False, want_key_block=False, stream=None):
+    """_calcPendingStates (tlsrecordlayer.py:1061-1149) for many connections
+    at once on the GPU.  conns: iterable of dicts with `secret` (48-byte
+    master secret, or premaster when premaster=True: calcMasterSecret
+    mathtls.py:70-82 runs first), `client_random`, `server_random`, `suite`,
+    `version`, `client` (bool) and optional `fixed_iv`.  Raises ValueError
+    (the reference's AssertionError paths) if any connection has an
+    unknown suite or version."""
+    from .device import DeviceBuffer, synchronize
+
+    conns = list(conns)
+    n = len(conns)
+    descs = (N.DeriveDesc * max(1, n))()
+    for i, c in enumerate(conns):
+        d = descs[i]
+        for field, size in (("secret", 48), ("client_random", 32), ("server_random", 32)):
+            v = bytes(c[field])
+            if len(v) != size:
+                raise ValueError("%s must be %d bytes" % (field, size))
+            ctypes.memmove(ctypes.addressof(d) + getattr(N.DeriveDesc, field).offset, v, size)
+        fiv = bytes(c.get("fixed_iv") or b"")[:16]
+        ctypes.memmove(ctypes.addressof(d) + N.DeriveDesc.fixed_iv.offset, fiv, len(fiv))
+        suite = c["suite"]
+        d.suite = SUITE_NAMES[suite] if isinstance(suite, str) else int(suite)
+        d.ver_major, d.ver_minor = tuple(c["version"])
+        d.client = 1 if c.get("client", True) else 0
+        d.flags = N.DERIVE_PREMASTER if premaster else 0
+    dd = DeviceBuffer(ctypes.sizeof(descs))
+    dd.upload(bytes(descs))
+    ws, rs = DeviceBuffer(n * N.CONN_STATE_BYTES), DeviceBuffer(n * N.CONN_STATE_BYTES)
+    ms = DeviceBuffer(n * 48)
+    kb = DeviceBuffer(n * N.KEY_BLOCK_MAX) if want_key_block else None
+    st = DeviceBuffer(4 * max(1, n))
+    N.call("tlsgpu_derive_states_dev", dd.ptr, n, ws.ptr, rs.ptr, ms.ptr, kb.ptr if kb else None, st.ptr,
+           stream.handle if stream else None)
+    if stream is None:
+        synchronize()
+    status = st.download(4 * n).view(np.int32)
+    if (status != 0).any():
+        bad = int(np.nonzero(status)[0][0])
+        raise ValueError("key derivation failed for connection %d (suite/version)" % bad)
+    master = ms.download(48 * n).reshape(n, 48)
+    key_block = kb.download().reshape(n, N.KEY_BLOCK_MAX) if kb else None
+    return DerivedStates(n, ws, rs, master, key_block, status)
 
 
 class RecordLayer:

@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include "tg_common.h"
 #include "tg_hash.h"
+#include "tg_keysched.h"
 #include "tg_launch.h"
 
 using namespace tg;
@@ -30,141 +31,23 @@ int fail(int code, const char* what) {
 
 constexpr AesTables h_aes{};
 
-inline uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
-inline uint32_t rotl(uint32_t x, int n) { return n ? (x << n) | (x >> (32 - n)) : x; }
-inline uint32_t le_word(const uint8_t* p) {
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
-}
-inline uint32_t be_word(const uint8_t* p) {
-    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | (uint32_t)p[3];
-}
-
-// FIPS-197 §5.2 key expansion; stored as LE column words (+ equivalent
-// inverse cipher keys, §5.3.5).  Same result as rijndael.py:206-276.
-void aes_expand(ConnState* st, const uint8_t* key, int klen) {
-    const int nk = klen / 4, nr = nk + 6, total = 4 * (nr + 1);
-    uint32_t w[60];
-    for (int i = 0; i < nk; i++) w[i] = be_word(key + 4 * i);
-    uint8_t rcon = 1;
-    for (int i = nk; i < total; i++) {
-        uint32_t t = w[i - 1];
-        if (i % nk == 0) {
-            t = ((uint32_t)h_aes.sbox[(t >> 16) & 0xff] << 24) | ((uint32_t)h_aes.sbox[(t >> 8) & 0xff] << 16) |
-                ((uint32_t)h_aes.sbox[t & 0xff] << 8) | h_aes.sbox[t >> 24];
-            t ^= (uint32_t)rcon << 24;
-            rcon = gf_mul(rcon, 2);
-        } else if (nk > 6 && i % nk == 4) {
-            t = ((uint32_t)h_aes.sbox[t >> 24] << 24) | ((uint32_t)h_aes.sbox[(t >> 16) & 0xff] << 16) |
-                ((uint32_t)h_aes.sbox[(t >> 8) & 0xff] << 8) | h_aes.sbox[t & 0xff];
-        }
-        w[i] = w[i - nk] ^ t;
-    }
-    for (int i = 0; i < total; i++) st->ek[i] = bswap(w[i]);
-    for (int r = 0; r <= nr; r++)
-        for (int c = 0; c < 4; c++) {
-            uint32_t x = st->ek[4 * (nr - r) + c];
-            if (r > 0 && r < nr)
-                x = h_aes.im0[x & 0xff] ^ rotl(h_aes.im0[(x >> 8) & 0xff], 8) ^
-                    rotl(h_aes.im0[(x >> 16) & 0xff], 16) ^ rotl(h_aes.im0[x >> 24], 24);
-            st->dk[4 * r + c] = x;
-        }
-}
-
-// FIPS 46-3 key schedule, packed for the kernels' rotated-domain rounds:
-// even word = K8 | K6<<8 | K4<<16 | K2<<24, odd word = K7 | K5<<8 | K3<<16 | K1<<24
-uint64_t permute_bits(uint64_t in, int inbits, const uint8_t* tab, int n) {
-    uint64_t out = 0;
-    for (int i = 0; i < n; i++) out = (out << 1) | ((in >> (inbits - tab[i])) & 1);
-    return out;
-}
-void des_schedule(uint32_t out[32], const uint8_t key[8]) {
-    uint64_t k = 0;
-    for (int i = 0; i < 8; i++) k = (k << 8) | key[i];
-    uint64_t cd = permute_bits(k, 64, DesConst::PC1, 56);
-    uint32_t c = (uint32_t)(cd >> 28) & 0xfffffff, d = (uint32_t)cd & 0xfffffff;
-    for (int r = 0; r < 16; r++) {
-        for (int s = 0; s < DesConst::SHIFTS[r]; s++) {
-            c = ((c << 1) | (c >> 27)) & 0xfffffff;
-            d = ((d << 1) | (d >> 27)) & 0xfffffff;
-        }
-        uint64_t sub = permute_bits(((uint64_t)c << 28) | d, 56, DesConst::PC2, 48);
-        uint32_t K[8];
-        for (int i = 0; i < 8; i++) K[i] = (uint32_t)(sub >> (42 - 6 * i)) & 63;
-        out[2 * r] = K[7] | (K[5] << 8) | (K[3] << 16) | (K[1] << 24);
-        out[2 * r + 1] = K[6] | (K[4] << 8) | (K[2] << 16) | (K[0] << 24);
-    }
-}
-
-// python_rc4.py:13-23
-void rc4_ksa(ConnState* st, const uint8_t* key, size_t klen) {
-    for (int i = 0; i < 256; i++) st->rc4_S[i] = (uint8_t)i;
-    uint32_t j = 0;
-    for (int i = 0; i < 256; i++) {
-        j = (j + st->rc4_S[i] + key[i % klen]) & 255;
-        uint8_t t = st->rc4_S[i];
-        st->rc4_S[i] = st->rc4_S[j];
-        st->rc4_S[j] = t;
-    }
-    st->rc4_i = st->rc4_j = 0;
-}
-
-template <int MAC>
-void midstate(uint32_t out[8], const uint8_t block[64]) {
-    using H = Hash<MAC>;
-    uint32_t h[8] = {0}, w[16];
-    H::init(h);
-    for (int i = 0; i < 16; i++) w[i] = H::BE ? be_word(block + 4 * i) : le_word(block + 4 * i);
-    H::compress(h, w);
-    for (int i = 0; i < 8; i++) out[i] = h[i];
-}
-void midstate_any(int mac, uint32_t out[8], const uint8_t block[64]) {
-    if (mac == TLSGPU_MAC_SHA1) midstate<TLSGPU_MAC_SHA1>(out, block);
-    else if (mac == TLSGPU_MAC_SHA256) midstate<TLSGPU_MAC_SHA256>(out, block);
-    else midstate<TLSGPU_MAC_MD5>(out, block);
-}
-
-void pack_le(uint32_t* dst, const uint8_t* src, size_t n) {
-    for (size_t i = 0; i < (n + 3) / 4; i++) {
-        uint32_t v = 0;
-        for (size_t b = 0; b < 4 && 4 * i + b < n; b++) v |= (uint32_t)src[4 * i + b] << (8 * b);
-        dst[i] = v;
-    }
-}
-
-int cipher_setup(ConnState* st, int cipher, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len) {
-    st->cipher = (uint32_t)cipher;
-    switch (cipher) {
-        case TLSGPU_CIPHER_AES128:
-        case TLSGPU_CIPHER_AES192:
-        case TLSGPU_CIPHER_AES256:
-            // aes.py:8-13
-            if (key_len != (cipher == TLSGPU_CIPHER_AES128 ? 16u : cipher == TLSGPU_CIPHER_AES192 ? 24u : 32u) ||
-                iv_len != 16 || !key || !iv)
-                return fail(TLSGPU_EINVAL, "AES needs a 16/24/32-byte key and a 16-byte IV");
-            aes_expand(st, key, (int)key_len);
-            st->bs = 16;
-            pack_le(st->iv, iv, 16);
-            break;
-        case TLSGPU_CIPHER_3DES:
-            // tripledes.py:8-13
-            if (key_len != 24 || iv_len != 8 || !key || !iv)
-                return fail(TLSGPU_EINVAL, "3DES needs a 24-byte key and an 8-byte IV");
-            for (int i = 0; i < 3; i++) des_schedule(st->des[i], key + 8 * i);
-            st->bs = 8;
-            pack_le(st->iv, iv, 8);
-            break;
-        case TLSGPU_CIPHER_RC4:
-            // rc4.py:9-10; cipherfactory.py:70-71
-            if (key_len < 16 || key_len > 256 || iv_len != 0 || !key)
-                return fail(TLSGPU_EINVAL, "RC4 needs a 16..256-byte key and no IV");
-            rc4_ksa(st, key, key_len);
-            st->bs = 0;
-            break;
-        default:
-            return fail(TLSGPU_EINVAL, "unknown cipher");
-    }
-    return 0;
-}
+const char* const KS_MSG[KS_NCODES] = {
+    "ok",
+    "no TLS suite uses AES-192",
+    "version must be (3,0)..(3,3)",
+    "unknown MAC",
+    "SHA256 suites need TLS 1.2",
+    "AES needs a 16/24/32-byte key and a 16-byte IV",
+    "3DES needs a 24-byte key and an 8-byte IV",
+    "RC4 needs a 16..256-byte key and no IV",
+    "unknown cipher",
+    "TLS>=1.1 block cipher needs fixed_iv of the block size",
+    "MAC key longer than 64 bytes",
+    "SSL3 SHA MAC key must be 20 bytes",
+    "SSL3 MD5 MAC key must be 16 bytes",
+    "SSL3 supports SHA1/MD5 MACs only",
+};
+int ks_fail(int code) { return code ? fail(TLSGPU_EINVAL, KS_MSG[code]) : 0; }
 
 inline ConnState* S(tlsgpu_conn_state* p) { return reinterpret_cast<ConnState*>(p); }
 inline const ConnState* S(const tlsgpu_conn_state* p) { return reinterpret_cast<const ConnState*>(p); }
@@ -282,57 +165,9 @@ int tlsgpu_conn_state_init(tlsgpu_conn_state* out, int cipher, int mac, int ver_
                            const uint8_t* mac_key, size_t mac_key_len, const uint8_t* fixed_iv,
                            size_t fixed_iv_len, uint64_t seqnum) {
     if (!out) return fail(TLSGPU_EINVAL, "null state");
-    if (cipher == TLSGPU_CIPHER_AES192) return fail(TLSGPU_EINVAL, "no TLS suite uses AES-192");
     memset(out, 0, sizeof *out);
-    ConnState* st = S(out);
-    if (ver_major != 3 || ver_minor < 0 || ver_minor > 3)
-        return fail(TLSGPU_EINVAL, "version must be (3,0)..(3,3)");  // handshakesettings.py:174-178
-    if (mac != TLSGPU_MAC_SHA1 && mac != TLSGPU_MAC_SHA256 && mac != TLSGPU_MAC_MD5)
-        return fail(TLSGPU_EINVAL, "unknown MAC");
-    if (mac == TLSGPU_MAC_SHA256 && ver_minor != 3)
-        return fail(TLSGPU_EINVAL, "SHA256 suites need TLS 1.2");  // constants.py:204-210
-    int rc = cipher_setup(st, cipher, key, key_len, iv, iv_len);
-    if (rc) return rc;
-    st->mac = (uint32_t)mac;
-    st->vmaj = (uint8_t)ver_major;
-    st->vmin = (uint8_t)ver_minor;
-    st->ssl3 = ver_minor == 0;
-    st->seqnum = seqnum;
-    st->maclen = (uint8_t)(mac == TLSGPU_MAC_SHA1 ? 20 : mac == TLSGPU_MAC_SHA256 ? 32 : 16);
-    st->explicit_iv = (ver_minor >= 2 && cipher != TLSGPU_CIPHER_RC4) ? 1u : 0u;
-    if (st->explicit_iv) {
-        if (!fixed_iv || fixed_iv_len != st->bs)
-            return fail(TLSGPU_EINVAL, "TLS>=1.1 block cipher needs fixed_iv of the block size");
-        pack_le(st->fixed_iv, fixed_iv, fixed_iv_len);
-    }
-    if (mac_key_len > 64 || (!mac_key && mac_key_len)) return fail(TLSGPU_EINVAL, "MAC key longer than 64 bytes");
-    st->mac_key_len = (uint32_t)mac_key_len;
-    if (st->ssl3) {
-        // MAC_SSL (mathtls.py:125-151): H(K | pad2 | H(K | pad1 | m)), pads 40 (SHA) / 48 (MD5) bytes
-        if (mac == TLSGPU_MAC_SHA1) {
-            if (mac_key_len != 20) return fail(TLSGPU_EINVAL, "SSL3 SHA MAC key must be 20 bytes");
-            for (int i = 0; i < 5; i++) st->mac_key[i] = be_word(mac_key + 4 * i);
-        } else if (mac == TLSGPU_MAC_MD5) {
-            if (mac_key_len != 16) return fail(TLSGPU_EINVAL, "SSL3 MD5 MAC key must be 16 bytes");
-            uint8_t blk[64];
-            memcpy(blk, mac_key, 16);
-            memset(blk + 16, 0x36, 48);
-            midstate_any(mac, st->mac_in, blk);
-            memset(blk + 16, 0x5c, 48);
-            midstate_any(mac, st->mac_out, blk);
-        } else {
-            return fail(TLSGPU_EINVAL, "SSL3 supports SHA1/MD5 MACs only");
-        }
-    } else {
-        // HMAC (RFC 2104) ipad/opad midstates, as hmac.HMAC does (mathtls.py:116-117)
-        uint8_t k[64] = {0}, blk[64];
-        if (mac_key_len) memcpy(k, mac_key, mac_key_len);
-        for (int i = 0; i < 64; i++) blk[i] = k[i] ^ 0x36;
-        midstate_any(mac, st->mac_in, blk);
-        for (int i = 0; i < 64; i++) blk[i] = k[i] ^ 0x5c;
-        midstate_any(mac, st->mac_out, blk);
-    }
-    return 0;
+    return ks_fail(build_conn_state(S(out), cipher, mac, ver_major, ver_minor, key, key_len, iv, iv_len, mac_key,
+                                    mac_key_len, fixed_iv, fixed_iv_len, seqnum, h_aes.sbox, h_aes.im0));
 }
 
 int tlsgpu_cipher_state_init(tlsgpu_conn_state* out, int cipher, const uint8_t* key, size_t key_len,
@@ -340,7 +175,7 @@ int tlsgpu_cipher_state_init(tlsgpu_conn_state* out, int cipher, const uint8_t* 
     if (!out) return fail(TLSGPU_EINVAL, "null state");
     memset(out, 0, sizeof *out);
     ConnState* st = S(out);
-    int rc = cipher_setup(st, cipher, key, key_len, iv, iv_len);
+    int rc = ks_fail(cipher_setup(st, cipher, key, key_len, iv, iv_len, h_aes.sbox, h_aes.im0));
     if (rc) return rc;
     st->raw = 1;
     return 0;
@@ -353,7 +188,7 @@ int tlsgpu_conn_state_set_seqnum(tlsgpu_conn_state* st, uint64_t seqnum) {
 int tlsgpu_conn_state_set_iv(tlsgpu_conn_state* st, const uint8_t* iv, size_t iv_len) {
     ConnState* s = S(st);
     if (iv_len != s->bs || !s->bs) return fail(TLSGPU_EINVAL, "IV length must equal the block size");
-    pack_le(s->iv, iv, iv_len);
+    ks_pack_le(s->iv, iv, iv_len);
     return 0;
 }
 int tlsgpu_conn_state_get_seqnum(const tlsgpu_conn_state* st, uint64_t* seqnum) {
@@ -561,6 +396,16 @@ int tlsgpu_open_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_o
                                next_epoch(), HS(s), &known);
     if (!known) return fail(TLSGPU_EINVAL, "unsupported open variant");
     if (e != hipSuccess) return fail_hip(e, "open launch");
+    return 0;
+}
+
+int tlsgpu_derive_states_dev(const tlsgpu_derive_desc* descs, uint32_t n, tlsgpu_conn_state* write_states,
+                             tlsgpu_conn_state* read_states, uint8_t* master_out, uint8_t* key_block_out,
+                             int32_t* status, tlsgpu_stream s) {
+    if (n && (!descs || !write_states || !read_states || !status)) return fail(TLSGPU_EINVAL, "null argument");
+    if (n > (1u << 26)) return fail(TLSGPU_EINVAL, "too many connections");
+    hipError_t e = launch_derive(descs, n, S(write_states), S(read_states), master_out, key_block_out, status, HS(s));
+    if (e != hipSuccess) return fail_hip(e, "derive launch");
     return 0;
 }
 

@@ -10,6 +10,7 @@
 #include "tg_aesq.h"
 #include "tg_aes3.h"
 #include "tg_open3.h"
+#include "tg_derive.h"
 #include "tg_launch.h"
 
 namespace tg {
@@ -708,6 +709,14 @@ hipError_t launch_cipher(int cipher, int dec, const tlsgpu_span* spans, uint32_t
 #undef TG_CIPHER_CASE
     *known = false;
     return hipSuccess;
+}
+
+hipError_t launch_derive(const tlsgpu_derive_desc* descs, uint32_t n, ConnState* ws, ConnState* rs,
+                         uint8_t* master_out, uint8_t* kb_out, int32_t* status, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(derive_kernel, dim3((n + 63) / 64), dim3(64), 0, s, descs, n, ws, rs, master_out, kb_out,
+                       status);
+    return hipGetLastError();
 }
 
 hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, hipStream_t s) {

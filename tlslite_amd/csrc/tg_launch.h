@@ -24,6 +24,8 @@ bool open_needs_workspace(uint32_t variant);
 hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
                        const tlsgpu_open_record* recs, uint32_t nrecords, const uint8_t* wire, uint8_t* pt,
                        ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known);
+hipError_t launch_derive(const tlsgpu_derive_desc* descs, uint32_t n, ConnState* ws, ConnState* rs,
+                         uint8_t* master_out, uint8_t* kb_out, int32_t* status, hipStream_t s);
 hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, hipStream_t s);
 
 }  // namespace tg

@@ -20,7 +20,7 @@ for c in cfg3 cfg4 cfg5; do
 done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
-    python3 $R/bench.py --no-check --no-cpu --no-host-inclusive --no-open --steps 50 > $O/bench_prof.json 2> $O/bench_prof.err \
+    python3 $R/bench.py --no-check --no-cpu --no-host-inclusive --no-open --no-derive --steps 50 > $O/bench_prof.json 2> $O/bench_prof.err \
     || { echo "rocprof failed"; tail -20 $O/bench_prof.err; exit 1; }
 grep '^{' $O/bench_prof.json | cut -c1-300
 echo done

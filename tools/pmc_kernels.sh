@@ -18,7 +18,7 @@ for G in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_
          "SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
          "FETCH_SIZE" "WRITE_SIZE"; do
   timeout -k 10 300 rocprofv3 --pmc $G --kernel-trace --output-format csv -d $OUT/g$i -o run -- \
-      python $R/bench.py --config $CFG --steps 3 --warmup 1 --no-check --no-cpu --no-host-inclusive --no-open "$@" > $OUT/g$i.log 2>&1
+      python $R/bench.py --config $CFG --steps 3 --warmup 1 --no-check --no-cpu --no-host-inclusive --no-open --no-derive "$@" > $OUT/g$i.log 2>&1
   i=$((i+1))
 done
 python $R/tools/pmc_summarize.py $OUT $CFG
