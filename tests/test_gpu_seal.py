@@ -171,6 +171,7 @@ AES_IMPLS = {
     "cbc1io16": {"TLSGPU_CBC_IO": "16"},          # cbc_kernel<NR, IO16>: 16-byte I/O + quad transposes
     "macquad": {"TLSGPU_MAC_LOAD": "quad"},       # mac_kernel<.., QL>: quad-cooperative loads
     "cbc2": {"TLSGPU_CBC_ILP": "2"},              # cbc2_kernel: two chains per quad
+    "pair": {"TLSGPU_CBC_LAYOUT": "pair"},        # cbcp_kernel: two lanes per chain
     "fused": {"TLSGPU_SEAL_IMPL": "fused"},       # single fused quad kernel
     "lane": {"TLSGPU_SEAL_IMPL": "lane"},         # one lane per chain
 }

@@ -677,4 +677,186 @@ cbc2_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tls
     if (hasB && B.any) sb->iv[q] = B.iv;
 }
 
+// ---------------------------------------------------------------------------
+// cbcp_kernel: 16 waves x 32 lane PAIRS, 2 lanes per chain, up to 512 chains per
+// workgroup.  Lane h holds AES state columns 2h and 2h+1: a round is 8 conflict-free
+// T-table lookups per lane; each lane XORs, for each of its columns, the two terms it
+// owns, and the two terms its partner needs (with the partner's round-key column
+// folded in) cross over in ONE DPP swap per column (tools/aes_layout_microbench.hip:
+// 84.9 ns/round at 256 chains per CU against 89.5 for the quad layout, 87 % of the
+// LDS lookup floor at 512 chains per CU).  Plaintext / ciphertext move as 8-byte
+// column pairs.  Same results as cbc_kernel.
+constexpr int CP_THREADS = 1024;
+constexpr int CP_CHAINS = 512;
+
+__device__ __forceinline__ uint32_t pair_swap(uint32_t v) {  // lane h <- lane h^1
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);
+}
+
+struct PairAes : QuadAes {
+    // column j of the next state = T0[b0(s_j)] ^ T1[b1(s_j+1)] ^ T2[b2(s_j+2)] ^ T3[b3(s_j+3)] ^ k_j;
+    // pk = the partner's key columns (round_keys_pair)
+    __device__ __forceinline__ void round(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
+        const uint32_t a2 = look<2, 2>(a), b3 = look<3, 3>(b), a1 = look<1, 1>(a), b2 = look<2, 2>(b);
+        const uint32_t a0 = look<0, 0>(a), b1 = look<1, 1>(b), b0 = look<0, 0>(b), a3 = look<3, 3>(a);
+        const uint32_t sA = __builtin_amdgcn_bitop3_b32(a2, b3, ka, 0x96);
+        const uint32_t sB = __builtin_amdgcn_bitop3_b32(a1, b2, kb, 0x96);
+        a = (a0 ^ b1) ^ pair_swap(sA);
+        b = (b0 ^ a3) ^ pair_swap(sB);
+    }
+    // final round: S-box byte B of s sits at byte B of table (B+2)&3
+    __device__ __forceinline__ void last(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
+        const uint32_t ta0 = look<2, 0>(a), tb1 = look<3, 1>(b), ta2 = look<0, 2>(a), tb3 = look<1, 3>(b);
+        const uint32_t tb0 = look<2, 0>(b), ta3 = look<1, 3>(a), ta1 = look<3, 1>(a), tb2 = look<0, 2>(b);
+        const uint32_t oA = perm(tb1, ta0, 0x0c0c0500u);
+        const uint32_t sA = perm(tb3, ta2, 0x07020c0cu) ^ ka;
+        const uint32_t oB = perm(ta3, tb0, 0x070c0c00u);
+        const uint32_t sB = perm(tb2, ta1, 0x0c06010cu) ^ kb;
+        a = oA ^ pair_swap(sA);
+        b = oB ^ pair_swap(sB);
+    }
+    // kw = own whitening columns; k[2r], k[2r+1] (r >= 1) = the partner's columns of round key r
+    template <int NR>
+    static __device__ __forceinline__ void round_keys(const uint32_t* ek, uint32_t h, uint32_t* k) {
+        const uint32_t ca = 2 * h, pa = 2 - ca;
+        k[0] = ek[ca];
+        k[1] = ek[ca + 1];
+#pragma unroll
+        for (int r = 1; r <= NR; r++) {
+            k[2 * r] = ek[4 * r + pa];
+            k[2 * r + 1] = ek[4 * r + pa + 1];
+        }
+    }
+    // one block whose input is already whitened
+    template <int NR>
+    __device__ __forceinline__ void encrypt_w(uint32_t& a, uint32_t& b, const uint32_t* k) const {
+#pragma unroll
+        for (int r = 1; r < NR; r++) round(a, b, k[2 * r], k[2 * r + 1]);
+        last(a, b, k[2 * NR], k[2 * NR + 1]);
+    }
+};
+
+template <bool AL>
+__device__ __forceinline__ uint2 ld64t(const uint8_t* p) {
+    if constexpr (AL) return *(const uint2*)p;
+    return make_uint2(ld32t<false>(p), ld32t<false>(p + 4));
+}
+template <bool AL>
+__device__ __forceinline__ void st64t(uint8_t* p, uint32_t a, uint32_t b) {
+    if constexpr (AL) {
+        *(uint2*)p = make_uint2(a, b);
+    } else {
+        st32t<false>(p, a);
+        st32t<false>(p + 4, b);
+    }
+}
+
+// CBC over nb full blocks (P / O include the lane's 8-byte column-pair offset); groups of
+// 8 blocks with the next group prefetched, index clamped to the last block (cbc_bulk).
+template <int NR, bool AL>
+__device__ __forceinline__ void cbcp_bulk(const PairAes& aes, const uint32_t* k, uint32_t& ia, uint32_t& ib,
+                                          const uint8_t* P, uint8_t* O, uint32_t nb) {
+    if (nb == 0) return;
+    const uint32_t last = nb - 1;
+    uint2 f[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) f[i] = ld64t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
+    uint32_t b0 = 0;
+    for (; b0 + 8 <= nb; b0 += 8) {
+        uint2 c[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) c[i] = f[i];
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t b = b0 + 8 + i;
+            f[i] = ld64t<AL>(P + 16 * (b < last ? b : last));
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            ia = __builtin_amdgcn_bitop3_b32(c[i].x, ia, k[0], 0x96);
+            ib = __builtin_amdgcn_bitop3_b32(c[i].y, ib, k[1], 0x96);
+            aes.encrypt_w<NR>(ia, ib, k);
+            st64t<AL>(O + 16 * (b0 + i), ia, ib);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        if (b0 + i < nb) {
+            ia = __builtin_amdgcn_bitop3_b32(f[i].x, ia, k[0], 0x96);
+            ib = __builtin_amdgcn_bitop3_b32(f[i].y, ib, k[1], 0x96);
+            aes.encrypt_w<NR>(ia, ib, k);
+            st64t<AL>(O + 16 * (b0 + i), ia, ib);
+        }
+    }
+}
+
+template <int NR>
+__global__ void __launch_bounds__(CP_THREADS, 1)
+cbcp_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
+            uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
+            ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,
+            uint32_t cpw, uint32_t epoch, uint32_t debug_skip) {
+    aes_lds_fill(nullptr, false);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t local = (threadIdx.x >> 6) * 32 + (lane >> 1);
+    const uint32_t h = lane & 1;
+    const uint32_t cid = blockIdx.x * cpw + local;
+    if (local >= cpw || cid >= nchains) return;  // both lanes of a pair leave together
+    const tlsgpu_chain ch = chains[cid];
+    ConnState* st = states + ch.state;
+    set_prio(prio_of(debug_skip, 4, 1));
+    PairAes aes;
+    aes.init();
+    uint32_t k[2 * (NR + 1)];
+    PairAes::round_keys<NR>(st->ek, h, k);
+    uint32_t ia = st->iv[2 * h], ib = st->iv[2 * h + 1];
+    const uint32_t fa = st->fixed_iv[2 * h], fb = st->fixed_iv[2 * h + 1];
+    const uint32_t E = st->explicit_iv ? 16u : 0u;
+    bool any = false;
+    for (uint32_t j = 0; j < ch.count; j++) {
+        const uint32_t r = ch.first + j;
+        if (r >= nrecords) break;
+        const RecMeta mt = meta[r];
+        if (mt.epoch != epoch || mt.status != 1) continue;
+        any = true;
+        const tlsgpu_record R = recs[r];
+        const uint32_t n = R.pt_len;
+        const uint8_t* P = pt + R.pt_off + 8 * h;
+        uint8_t* B = wire + R.wire_off + 5;
+        const bool al8 = (((uintptr_t)(pt + R.pt_off) | (uintptr_t)B) & 7) == 0;
+        const bool al4 = (((uintptr_t)(pt + R.pt_off) | (uintptr_t)B) & 3) == 0;
+        if (E) {  // E_K(fixedIVBlock ^ residue) (tlsrecordlayer.py:594-595)
+            ia = fa ^ ia ^ k[0];
+            ib = fb ^ ib ^ k[1];
+            aes.encrypt_w<NR>(ia, ib, k);
+            st32(B + 8 * h, ia, al4);
+            st32(B + 8 * h + 4, ib, al4);
+        }
+        uint8_t* O = B + E + 8 * h;
+        const uint32_t nb = (debug_skip & 1) ? 0u : (n >> 4);
+        if (al8)
+            cbcp_bulk<NR, true>(aes, k, ia, ib, P, O, nb);
+        else
+            cbcp_bulk<NR, false>(aes, k, ia, ib, P, O, nb);
+        // tail blocks from the MAC kernel's slot
+        const uint32_t r16 = n & 15;
+        const uint8_t* slot = tails + (size_t)r * TAIL_SLOT + 8 * h;
+        uint8_t* Ot = B + E + (n - r16) + 8 * h;
+        const uint32_t T = mt.tail_len;
+        for (uint32_t off = 0; off < T; off += 16) {
+            const uint2 t = *(const uint2*)(slot + off);
+            ia = t.x ^ ia ^ k[0];
+            ib = t.y ^ ib ^ k[1];
+            aes.encrypt_w<NR>(ia, ib, k);
+            st32(Ot + off, ia, al4);
+            st32(Ot + off + 4, ib, al4);
+        }
+    }
+    if (any) {
+        st->iv[2 * h] = ia;
+        st->iv[2 * h + 1] = ib;
+    }
+}
+
 }  // namespace tg

@@ -528,6 +528,25 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
     // (8 waves, 2 chains per quad)
     const char* ilp_env = getenv("TLSGPU_CBC_ILP");
     const int ilp = (ilp_env && atoi(ilp_env) == 2) ? 2 : 1;
+    // TLSGPU_CBC_LAYOUT (read per launch): "pair" = cbcp_kernel (2 lanes per chain, up to 512
+    // chains per CU; A/B only: 5 % slower on cfg2, 8 % on cfg3, same box), otherwise the quad
+    // layout cbc_kernel / cbc2_kernel (4 lanes per chain)
+    const char* lay_env = getenv("TLSGPU_CBC_LAYOUT");
+    const bool quad = !(lay_env && lay_env[0] == 'p') || ilp == 2 || env_is("TLSGPU_CBC_IO", '1');
+    if (!quad) {
+        uint32_t pw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
+        pw = pw < 1 ? 1 : (pw > (uint32_t)CP_CHAINS ? (uint32_t)CP_CHAINS : pw);
+        auto kern = cbcp_kernel<NR>;
+        static bool attrp = false;
+        if (!attrp) {
+            hipError_t e = set_lds(kern, AES_LDS_BYTES);
+            if (e != hipSuccess) return e;
+            attrp = true;
+        }
+        hipLaunchKernelGGL(kern, dim3((nchains + pw - 1) / pw), dim3(CP_THREADS), AES_LDS_BYTES, s, chains, nchains,
+                           recs, nrecords, pt, wire, states, meta, tails, pw, epoch, debug_skip_flags());
+        return hipGetLastError();
+    }
     uint32_t cpw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
     cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
     if (ilp == 2) {
