@@ -7,7 +7,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libtlsgpu.so")
+# TLSGPU_LIB: an alternative build of the same library (A/B timing tools only)
+LIB_PATH = os.environ.get("TLSGPU_LIB") or os.path.join(HERE, "lib", "libtlsgpu.so")
 
 # constants mirrored from include/tlsgpu.h
 CIPHER_AES128, CIPHER_AES256, CIPHER_RC4, CIPHER_3DES, CIPHER_AES192 = 1, 2, 3, 4, 5
@@ -116,6 +117,8 @@ def _load():
                           % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
     for name, res, args in SIGNATURES:
+        if os.environ.get("TLSGPU_LIB") and not hasattr(lib, name):
+            continue  # an older A/B build may predate a symbol; the in-tree library must have all
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
