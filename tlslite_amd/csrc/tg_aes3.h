@@ -61,8 +61,9 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
     const bool ok = st->cipher == (uint32_t)CIPHER_ID && st->mac == (uint32_t)MAC &&
                     st->ssl3 == (SSL3 ? 1u : 0u) && !st->raw;
     constexpr int DL = Hash<MAC>::DLEN;
+    constexpr uint32_t BS = CIPHER_ID == TLSGPU_CIPHER_3DES ? 8u : 16u;
     uint64_t seq = st->seqnum;
-    const uint32_t E = st->explicit_iv ? 16u : 0u;
+    const uint32_t E = st->explicit_iv ? BS : 0u;
     for (uint32_t k = 0; k < ch.count; k++) {
         const uint32_t r = ch.first + k;
         if (r >= nrecords) break;
@@ -78,15 +79,15 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
         } else {
             const uint32_t n = recs[r].pt_len;
             const uint32_t cur = E + n + DL;
-            const uint32_t body = cur + (16 - (cur & 15));
+            const uint32_t body = cur + (BS - (cur & (BS - 1)));
             if (n == 0) {
                 wire_len[r] = 0;
             } else if (body > 0xffffu) {
                 wire_len[r] = TLSGPU_ETOOBIG;
             } else {
-                const uint32_t r16 = n & 15;
+                const uint32_t rb = n & (BS - 1);
                 m.status = 1;
-                m.tail_len = r16 + DL + 16 - ((r16 + DL) & 15);
+                m.tail_len = rb + DL + BS - ((rb + DL) & (BS - 1));
                 seq++;
             }
         }
@@ -205,7 +206,7 @@ __device__ __forceinline__ void mac_bulk_quad(M& mac, const uint8_t* P, uint32_t
 // QL: quad-cooperative plaintext loads (mac_bulk_quad) where a quad allows them; a
 // separate instantiation so the default kernel keeps its small register footprint
 // (a MAC wave must fit beside four cbc_kernel waves on a SIMD: 4 x 96 + 128 <= 512 VGPRs)
-template <int MAC, bool SSL3, bool QL = false>
+template <int MAC, bool SSL3, bool QL = false, int BS = 16>
 __global__ void __launch_bounds__(256) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
                                                  const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
                                                  const ConnState* __restrict__ states, int32_t* __restrict__ wire_len,
@@ -249,9 +250,9 @@ __global__ void __launch_bounds__(256) mac_kernel(const tlsgpu_record* __restric
         else mac_bulk<false>(mac, P, nfull);
     }
     if (!act) return;
-    const uint32_t E = st->explicit_iv ? 16u : 0u;
+    const uint32_t E = st->explicit_iv ? (uint32_t)BS : 0u;
     const uint32_t cur0 = E + n + DL;
-    const uint32_t body = cur0 + (16 - (cur0 & 15));
+    const uint32_t body = cur0 + (BS - (cur0 & (BS - 1)));
     uint8_t* W = wire + R.wire_off;
     const uint32_t nf = n >> 6, r64 = n & 63;
     uint32_t tail[16];
@@ -259,11 +260,11 @@ __global__ void __launch_bounds__(256) mac_kernel(const tlsgpu_record* __restric
     uint32_t m[8];
     mac.finish(tail, (int)r64, n, st, m);
     if (R.flags & TLSGPU_FAULT_BAD_MAC) m[0] = (m[0] & ~0xffu) | ((m[0] + 1u) & 0xffu);
-    // CBC tail: P[16*nb ..) | MAC | pad  (tlsrecordlayer.py:597-606), built as dwords
+    // CBC tail: P[BS*nb ..) | MAC | pad  (tlsrecordlayer.py:597-606), built as dwords
     uint8_t* slot = tails + (size_t)r * TAIL_SLOT;
-    const uint32_t r16 = n & 15;
+    const uint32_t r16 = n & (BS - 1);
     const uint8_t* Pt = P + (n - r16);
-    const uint32_t padl = 15 - ((r16 + DL) & 15);
+    const uint32_t padl = (BS - 1) - ((r16 + DL) & (BS - 1));
     const uint32_t T = r16 + DL + padl + 1;
     uint32_t out[16];
 #pragma unroll
@@ -857,6 +858,136 @@ cbcp_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tls
         st->iv[2 * h] = ia;
         st->iv[2 * h + 1] = ib;
     }
+}
+
+// ---------------------------------------------------------------------------
+// tdes8_kernel: 3DES-EDE-CBC (openssl_tripledes.py:23, FIPS 46-3) with 8 lanes per
+// chain.  Lane j of a chain's 8-lane group evaluates ONE of the eight SP-box terms of
+// the Feistel function (a rotate, a key XOR, a 6-bit extract and one conflict-free LDS
+// lookup) and three DPP XOR steps (quad [1,0,3,2], quad [2,3,0,1], half-row mirror) sum
+// the eight terms in every lane of the group, so a round's critical path is one
+// lookup + three XORs instead of one lane issuing all eight lookups and their XOR chain.
+// The (l, r) halves are replicated in the group's lanes; lanes 0/1 store the two
+// ciphertext words.  128 chains per 1024-thread workgroup.  The MAC, the tail slot and
+// the header come from prefix_kernel / mac_kernel<.., 8> as for AES.
+constexpr int D8_THREADS = 1024;
+constexpr int D8_CHAINS = D8_THREADS / 8;
+
+struct Des8 {
+    uint32_t base, sh, rot;
+    __device__ __forceinline__ void init() {
+        const uint32_t lane = __lane_id(), j = lane & 7;
+        // SP table of each lane: j < 4 take bytes 0..3 of w = r ^ k_even (tables 7,5,3,1),
+        // j >= 4 bytes 0..3 of v = rotr4(r) ^ k_odd (tables 6,4,2,0) -- des_rounds()
+        const uint32_t K = j < 4 ? 7 - 2 * j : 6 - 2 * (j - 4);
+        base = (lane & 31) * 4 + K * 8192;
+        sh = 8 * (j & 3);
+        rot = j < 4 ? 0u : 4u;
+    }
+    __device__ __forceinline__ uint32_t f(uint32_t r, uint32_t kw) const {
+        const uint32_t t = __builtin_amdgcn_alignbit(r, r, rot) ^ kw;
+        const uint32_t idx = __builtin_amdgcn_ubfe(t, sh, 6);
+        uint32_t v = lds_read32((idx << 7) + base);
+        v ^= quad_dpp<0xB1>(v);
+        v ^= quad_dpp<0x4E>(v);
+        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
+        return v;
+    }
+    // block as two big-endian words; kw[16p + i] = this lane's key word of pass p, round i
+    __device__ __forceinline__ void block(uint32_t& hi, uint32_t& lo, const uint32_t* kw) const {
+        uint32_t l = hi, r = lo;
+        des_ip(l, r);
+#pragma unroll
+        for (int p = 0; p < 3; p++) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint32_t t = l ^ f(r, kw[16 * p + i]);
+                l = r;
+                r = t;
+            }
+            const uint32_t t = l;
+            l = r;
+            r = t;
+        }
+        des_fp(l, r);
+        hi = l;
+        lo = r;
+    }
+    // CBC on LE words (TdesCbc::enc_block): c = E(p ^ iv), iv = c
+    __device__ __forceinline__ void cbc(uint32_t d0, uint32_t d1, uint32_t& iv0, uint32_t& iv1,
+                                        const uint32_t* kw) const {
+        uint32_t hi = bswap32(d0 ^ iv0), lo = bswap32(d1 ^ iv1);
+        block(hi, lo, kw);
+        iv0 = bswap32(hi);
+        iv1 = bswap32(lo);
+    }
+};
+
+__global__ void __launch_bounds__(D8_THREADS, 1)
+tdes8_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
+             uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
+             ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,
+             uint32_t cpw, uint32_t epoch) {
+    // SP tables at LDS offset 0 (the kernel's only LDS), read back by absolute address (Des8::f)
+    extern __shared__ __attribute__((aligned(16))) uint32_t d8_lds[];
+    des_lds_fill(d8_lds);
+    __syncthreads();
+    const uint32_t j = threadIdx.x & 7;
+    const uint32_t local = threadIdx.x >> 3;
+    const uint32_t cid = blockIdx.x * cpw + local;
+    if (local >= cpw || cid >= nchains) return;  // the 8 lanes of a chain leave together
+    const tlsgpu_chain ch = chains[cid];
+    ConnState* st = states + ch.state;
+    Des8 D;
+    D.init();
+    uint32_t kw[48];
+#pragma unroll
+    for (int p = 0; p < 3; p++)
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int k = p == 1 ? 15 - i : i;  // EDE: the middle pass decrypts (keys backwards)
+            kw[16 * p + i] = st->des[p][2 * k + (j >= 4 ? 1 : 0)];
+        }
+    uint32_t iv0 = st->iv[0], iv1 = st->iv[1];
+    const uint32_t f0 = st->fixed_iv[0], f1 = st->fixed_iv[1];
+    const uint32_t E = st->explicit_iv ? 8u : 0u;
+    bool any = false;
+    for (uint32_t q = 0; q < ch.count; q++) {
+        const uint32_t r = ch.first + q;
+        if (r >= nrecords) break;
+        const RecMeta mt = meta[r];
+        if (mt.epoch != epoch || mt.status != 1) continue;
+        any = true;
+        const tlsgpu_record R = recs[r];
+        const uint32_t n = R.pt_len;
+        const uint8_t* P = pt + R.pt_off;
+        uint8_t* B = wire + R.wire_off + 5;
+        const bool al = (((uintptr_t)P | (uintptr_t)B) & 3) == 0;
+        if (E) {  // E_K(fixedIVBlock ^ residue) (tlsrecordlayer.py:594-595)
+            D.cbc(f0, f1, iv0, iv1, kw);
+            if (j < 2) st32(B + 4 * j, j ? iv1 : iv0, al);
+        }
+        uint8_t* O = B + E;
+        const uint32_t nb = n >> 3;
+        uint32_t n0 = ld32(P, al), n1 = ld32(P + 4, al);
+        for (uint32_t b = 0; b < nb; b++) {
+            const uint32_t d0 = n0, d1 = n1;
+            const uint32_t bn = b + 1 < nb ? b + 1 : b;  // prefetch, clamped to the last block
+            n0 = ld32(P + 8 * bn, al);
+            n1 = ld32(P + 8 * bn + 4, al);
+            D.cbc(d0, d1, iv0, iv1, kw);
+            if (j < 2) st32(O + 8 * b + 4 * j, j ? iv1 : iv0, al);
+        }
+        // tail blocks from the MAC kernel's slot
+        const uint8_t* slot = tails + (size_t)r * TAIL_SLOT;
+        uint8_t* Ot = O + 8 * nb;
+        const uint32_t T = mt.tail_len;
+        for (uint32_t off = 0; off < T; off += 8) {
+            D.cbc(*(const uint32_t*)(slot + off), *(const uint32_t*)(slot + off + 4), iv0, iv1, kw);
+            if (j < 2) st32(Ot + off + 4 * j, j ? iv1 : iv0, al);
+        }
+    }
+    if (any && j < 2) st->iv[j] = j ? iv1 : iv0;
 }
 
 }  // namespace tg

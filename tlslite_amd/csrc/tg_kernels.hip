@@ -504,14 +504,17 @@ template <int NR, int MAC, bool SSL3>
 static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
                                    int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s) {
-    constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : TLSGPU_CIPHER_AES256;
+    // NR 0 = 3DES (8-byte blocks)
+    constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
+    constexpr int BS = NR == 0 ? 8 : 16;
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
     hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(RecMeta), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((prefix_kernel<CID, MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains,
                        recs, states, wire_len, meta, nrecords, epoch);
-    auto mk = env_is("TLSGPU_MAC_LOAD", 'q') ? mac_kernel<MAC, SSL3, true> : mac_kernel<MAC, SSL3, false>;
+    auto mk = (BS == 16 && env_is("TLSGPU_MAC_LOAD", 'q')) ? mac_kernel<MAC, SSL3, true, BS>
+                                                           : mac_kernel<MAC, SSL3, false, BS>;
     hipLaunchKernelGGL(mk, dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords, pt, wire, states, wire_len,
                        meta, tails, epoch, debug_skip_flags());
     return hipGetLastError();
@@ -524,54 +527,68 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
                                    uint8_t* ws, uint32_t epoch, hipStream_t s) {
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
-    // TLSGPU_CBC_ILP (read per launch): 1 = cbc_kernel (16 waves, 1 chain per quad), 2 = cbc2_kernel
-    // (8 waves, 2 chains per quad)
-    const char* ilp_env = getenv("TLSGPU_CBC_ILP");
-    const int ilp = (ilp_env && atoi(ilp_env) == 2) ? 2 : 1;
-    // TLSGPU_CBC_LAYOUT (read per launch): "pair" = cbcp_kernel (2 lanes per chain, up to 512
-    // chains per CU; A/B only: 5 % slower on cfg2, 8 % on cfg3, same box), otherwise the quad
-    // layout cbc_kernel / cbc2_kernel (4 lanes per chain)
-    const char* lay_env = getenv("TLSGPU_CBC_LAYOUT");
-    const bool quad = !(lay_env && lay_env[0] == 'p') || ilp == 2 || env_is("TLSGPU_CBC_IO", '1');
-    if (!quad) {
+    if constexpr (NR == 0) {  // 3DES: 8 lanes per chain
         uint32_t pw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
-        pw = pw < 1 ? 1 : (pw > (uint32_t)CP_CHAINS ? (uint32_t)CP_CHAINS : pw);
-        auto kern = cbcp_kernel<NR>;
-        static bool attrp = false;
-        if (!attrp) {
+        pw = pw < 1 ? 1 : (pw > (uint32_t)D8_CHAINS ? (uint32_t)D8_CHAINS : pw);
+        static bool attrd = false;
+        if (!attrd) {
+            hipError_t e = set_lds(tdes8_kernel, DES_LDS_BYTES);
+            if (e != hipSuccess) return e;
+            attrd = true;
+        }
+        hipLaunchKernelGGL(tdes8_kernel, dim3((nchains + pw - 1) / pw), dim3(D8_THREADS), DES_LDS_BYTES, s, chains,
+                           nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch);
+        return hipGetLastError();
+    } else {
+        // TLSGPU_CBC_ILP (read per launch): 1 = cbc_kernel (16 waves, 1 chain per quad), 2 = cbc2_kernel
+        // (8 waves, 2 chains per quad)
+        const char* ilp_env = getenv("TLSGPU_CBC_ILP");
+        const int ilp = (ilp_env && atoi(ilp_env) == 2) ? 2 : 1;
+        // TLSGPU_CBC_LAYOUT (read per launch): "pair" = cbcp_kernel (2 lanes per chain, up to 512
+        // chains per CU; A/B only: 5 % slower on cfg2, 8 % on cfg3, same box), otherwise the quad
+        // layout cbc_kernel / cbc2_kernel (4 lanes per chain)
+        const char* lay_env = getenv("TLSGPU_CBC_LAYOUT");
+        const bool quad = !(lay_env && lay_env[0] == 'p') || ilp == 2 || env_is("TLSGPU_CBC_IO", '1');
+        if (!quad) {
+            uint32_t pw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
+            pw = pw < 1 ? 1 : (pw > (uint32_t)CP_CHAINS ? (uint32_t)CP_CHAINS : pw);
+            auto kern = cbcp_kernel<NR>;
+            static bool attrp = false;
+            if (!attrp) {
+                hipError_t e = set_lds(kern, AES_LDS_BYTES);
+                if (e != hipSuccess) return e;
+                attrp = true;
+            }
+            hipLaunchKernelGGL(kern, dim3((nchains + pw - 1) / pw), dim3(CP_THREADS), AES_LDS_BYTES, s, chains, nchains,
+                               recs, nrecords, pt, wire, states, meta, tails, pw, epoch, debug_skip_flags());
+            return hipGetLastError();
+        }
+        uint32_t cpw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
+        cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
+        if (ilp == 2) {
+            auto kern = cbc2_kernel<NR>;
+            static bool attr2 = false;
+            if (!attr2) {
+                hipError_t e = set_lds(kern, AES_LDS_BYTES);
+                if (e != hipSuccess) return e;
+                attr2 = true;
+            }
+            hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C2_THREADS), AES_LDS_BYTES, s, chains, nchains,
+                               recs, nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
+            return hipGetLastError();
+        }
+        const bool io16 = env_is("TLSGPU_CBC_IO", '1');
+        auto kern = io16 ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
+        static bool attr[2] = {false, false};
+        if (!attr[io16]) {
             hipError_t e = set_lds(kern, AES_LDS_BYTES);
             if (e != hipSuccess) return e;
-            attrp = true;
+            attr[io16] = true;
         }
-        hipLaunchKernelGGL(kern, dim3((nchains + pw - 1) / pw), dim3(CP_THREADS), AES_LDS_BYTES, s, chains, nchains,
-                           recs, nrecords, pt, wire, states, meta, tails, pw, epoch, debug_skip_flags());
+        hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C3_THREADS), AES_LDS_BYTES, s, chains, nchains, recs,
+                           nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
         return hipGetLastError();
     }
-    uint32_t cpw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
-    cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
-    if (ilp == 2) {
-        auto kern = cbc2_kernel<NR>;
-        static bool attr2 = false;
-        if (!attr2) {
-            hipError_t e = set_lds(kern, AES_LDS_BYTES);
-            if (e != hipSuccess) return e;
-            attr2 = true;
-        }
-        hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C2_THREADS), AES_LDS_BYTES, s, chains, nchains,
-                           recs, nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
-        return hipGetLastError();
-    }
-    const bool io16 = env_is("TLSGPU_CBC_IO", '1');
-    auto kern = io16 ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
-    static bool attr[2] = {false, false};
-    if (!attr[io16]) {
-        hipError_t e = set_lds(kern, AES_LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr[io16] = true;
-    }
-    hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C3_THREADS), AES_LDS_BYTES, s, chains, nchains, recs,
-                       nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
-    return hipGetLastError();
 }
 
 template <int NR, int MAC, bool SSL3>
@@ -610,6 +627,8 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
     TG_PH(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false)
     TG_PH(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)
     TG_PH(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)
+    TG_PH(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, false)
+    TG_PH(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, true)
 #undef TG_PH
     *known = false;
     return hipSuccess;
@@ -648,6 +667,11 @@ static hipError_t launch_seal_t(const tlsgpu_chain* chains, uint32_t nchains, co
         if (aes_impl() == 1)
             return launch_seal_aesq<NR, MAC, SSL3>(chains, nchains, recs, pt, wire, states, wire_len, s);
     }
+    if constexpr (CipherTraits<C>::ID == TLSGPU_CIPHER_3DES) {
+        if (aes_impl() == 0)  // split: prefix / MAC / 8-lane 3DES (TLSGPU_SEAL_IMPL=lane: one lane per chain)
+            return launch_seal_split<0, MAC, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,
+                                                   epoch, s);
+    }
     auto kern = seal_kernel<C, MAC, SSL3>;
     constexpr uint32_t lds = CipherTraits<C>::LDS;
     static bool attr = false;
@@ -663,7 +687,7 @@ static hipError_t launch_seal_t(const tlsgpu_chain* chains, uint32_t nchains, co
 
 bool seal_needs_workspace(uint32_t variant) {
     const uint32_t c = variant & 0xff;
-    return aes_impl() == 0 && (c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256);
+    return aes_impl() == 0 && (c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256 || c == TLSGPU_CIPHER_3DES);
 }
 
 hipError_t launch_seal(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
