@@ -874,40 +874,50 @@ constexpr int D8_THREADS = 1024;
 constexpr int D8_CHAINS = D8_THREADS / 8;
 
 struct Des8 {
-    uint32_t base, sh, rot;
+    uint32_t base, sa;
+    bool odd;
     __device__ __forceinline__ void init() {
         const uint32_t lane = __lane_id(), j = lane & 7;
         // SP table of each lane: j < 4 take bytes 0..3 of w = r ^ k_even (tables 7,5,3,1),
-        // j >= 4 bytes 0..3 of v = rotr4(r) ^ k_odd (tables 6,4,2,0) -- des_rounds()
+        // j >= 4 bytes 0..3 of v = rotr4(r) ^ k_odd = rotr4(r ^ rotl4(k_odd)) (tables 6,4,2,0)
+        // -- des_rounds()
         const uint32_t K = j < 4 ? 7 - 2 * j : 6 - 2 * (j - 4);
         base = (lane & 31) * 4 + K * 8192;
-        sh = 8 * (j & 3);
-        rot = j < 4 ? 0u : 4u;
+        odd = j >= 4;
+        // rotate so that the lane's 6 index bits (bit (j>=4 ? 4 : 0) + 8*(j&3) of t) land at bits 7..12
+        sa = ((odd ? 4u : 0u) + 8 * (j & 3) + 25u) & 31u;
     }
-    __device__ __forceinline__ uint32_t f(uint32_t r, uint32_t kw) const {
-        const uint32_t t = __builtin_amdgcn_alignbit(r, r, rot) ^ kw;
-        const uint32_t idx = __builtin_amdgcn_ubfe(t, sh, 6);
-        uint32_t v = lds_read32((idx << 7) + base);
+    // this lane's key word for the SP lookup (odd words pre-rotated, see init)
+    __device__ __forceinline__ uint32_t key(uint32_t even, uint32_t oddw) const {
+        return odd ? ((oddw << 4) | (oddw >> 28)) : even;
+    }
+    // Feistel f of t = r ^ key, summed over the 8 lanes of the group
+    __device__ __forceinline__ uint32_t f(uint32_t t) const {
+        const uint32_t u = __builtin_amdgcn_alignbit(t, t, sa);
+        uint32_t v = lds_read32((u & 0x1f80u) | base);
         v ^= quad_dpp<0xB1>(v);
         v ^= quad_dpp<0x4E>(v);
         v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
         return v;
     }
-    // block as two big-endian words; kw[16p + i] = this lane's key word of pass p, round i
+    // block as two big-endian words; kw[16p + i] = this lane's key word of pass p, round i.
+    // The next round's t = r' ^ k = l ^ f ^ k is one 3-input XOR off the critical path's f.
     __device__ __forceinline__ void block(uint32_t& hi, uint32_t& lo, const uint32_t* kw) const {
         uint32_t l = hi, r = lo;
         des_ip(l, r);
+        uint32_t t = r ^ kw[0];
 #pragma unroll
-        for (int p = 0; p < 3; p++) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint32_t t = l ^ f(r, kw[16 * p + i]);
+        for (int g = 0; g < 48; g++) {
+            const uint32_t fv = f(t);
+            const uint32_t rn = l ^ fv;
+            if (g % 16 != 15) {
+                if (g + 1 < 48) t = __builtin_amdgcn_bitop3_b32(l, fv, kw[g + 1], 0x96);
                 l = r;
-                r = t;
+                r = rn;
+            } else {  // end of a DES pass: (l, r) = (R16, L16) feeds the next pass
+                l = rn;
+                if (g + 1 < 48) t = r ^ kw[g + 1];
             }
-            const uint32_t t = l;
-            l = r;
-            r = t;
         }
         des_fp(l, r);
         hi = l;
@@ -946,7 +956,7 @@ tdes8_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             const int k = p == 1 ? 15 - i : i;  // EDE: the middle pass decrypts (keys backwards)
-            kw[16 * p + i] = st->des[p][2 * k + (j >= 4 ? 1 : 0)];
+            kw[16 * p + i] = D.key(st->des[p][2 * k], st->des[p][2 * k + 1]);
         }
     uint32_t iv0 = st->iv[0], iv1 = st->iv[1];
     const uint32_t f0 = st->fixed_iv[0], f1 = st->fixed_iv[1];
