@@ -2,6 +2,7 @@
 // include/tlsgpu.h).  Host-side connection-state construction (the
 // _calcPendingStates equivalent, tlsrecordlayer.py:1061-1149), memory /
 // stream / event plumbing, and argument validation in front of the kernels.
+#include <stdlib.h>
 #include <string.h>
 #include <stdio.h>
 #include "tg_common.h"
@@ -286,6 +287,7 @@ int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_r
 struct tlsgpu_pipeline_s {
     int dev;
     hipStream_t mac_s, cbc_s;
+    int cbc_cus;  // CUs of the cipher stream's mask (0 = all)
     hipEvent_t mac_done[2], cbc_done[2];
     void* ws[2];
     size_t ws_bytes;
@@ -296,8 +298,29 @@ int tlsgpu_pipeline_create(tlsgpu_pipeline* out, uint32_t max_records) {
     if (!out) return fail(TLSGPU_EINVAL, "null");
     tlsgpu_pipeline p = new tlsgpu_pipeline_s();
     TG_HIP(hipGetDevice(&p->dev));
-    TG_HIP(hipStreamCreateWithFlags(&p->mac_s, hipStreamNonBlocking));
-    TG_HIP(hipStreamCreateWithFlags(&p->cbc_s, hipStreamNonBlocking));
+    // TLSGPU_PIPE_MAC_CUS=N (experiment): the MAC phase on N CUs, the cipher phase on the rest
+    // (CU-masked streams, every k-th CU to the MAC side) instead of both sharing every CU
+    int ncu = 0;
+    TG_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->dev));
+    const char* mc = getenv("TLSGPU_PIPE_MAC_CUS");
+    const int nmac = mc ? atoi(mc) : 0;
+    p->cbc_cus = 0;
+    if (nmac > 0 && nmac < ncu && ncu <= 1024) {
+        uint32_t mmask[32] = {0}, cmask[32] = {0};
+        const int words = (ncu + 31) / 32;
+        int taken = 0;
+        for (int i = 0; i < ncu; i++) {
+            const bool mac = taken < nmac && (long)i * nmac / ncu != (long)(i + 1) * nmac / ncu;
+            if (mac) taken++;
+            (mac ? mmask : cmask)[i / 32] |= 1u << (i % 32);
+        }
+        TG_HIP(hipExtStreamCreateWithCUMask(&p->mac_s, (uint32_t)words, mmask));
+        TG_HIP(hipExtStreamCreateWithCUMask(&p->cbc_s, (uint32_t)words, cmask));
+        p->cbc_cus = ncu - taken;
+    } else {
+        TG_HIP(hipStreamCreateWithFlags(&p->mac_s, hipStreamNonBlocking));
+        TG_HIP(hipStreamCreateWithFlags(&p->cbc_s, hipStreamNonBlocking));
+    }
     for (int i = 0; i < 2; i++) {
         TG_HIP(hipEventCreateWithFlags(&p->mac_done[i], hipEventDisableTiming));
         TG_HIP(hipEventCreateWithFlags(&p->cbc_done[i], hipEventDisableTiming));
@@ -349,7 +372,7 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain* chains, uint32_t
         e = launch_seal_phases(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len,
                                static_cast<uint8_t*>(p->ws[i]), epoch, p->mac_s, p->mac_done[i], p->cbc_s,
                                reinterpret_cast<hipEvent_t>(cipher_start), reinterpret_cast<hipEvent_t>(cipher_stop),
-                               &known);
+                               &known, p->cbc_cus);
     } else {
         // single-kernel variants run on the cipher stream, in order with earlier calls
         if (cipher_start) TG_HIP(hipEventRecord(reinterpret_cast<hipEvent_t>(cipher_start), p->cbc_s));

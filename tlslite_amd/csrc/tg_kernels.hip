@@ -524,11 +524,13 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
 template <int NR>
 static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
-                                   uint8_t* ws, uint32_t epoch, hipStream_t s) {
+                                   uint8_t* ws, uint32_t epoch, hipStream_t s, int cus = 0) {
+    // cus > 0: the stream is CU-masked to that many CUs (pipeline with TLSGPU_PIPE_MAC_CUS)
+    const uint32_t ncu = cus > 0 ? (uint32_t)cus : (uint32_t)cu_count();
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
     if constexpr (NR == 0) {  // 3DES: 8 lanes per chain
-        uint32_t pw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
+        uint32_t pw = (nchains + ncu - 1) / ncu;
         pw = pw < 1 ? 1 : (pw > (uint32_t)D8_CHAINS ? (uint32_t)D8_CHAINS : pw);
         static bool attrd = false;
         if (!attrd) {
@@ -548,9 +550,10 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         // chains per CU; A/B only: 5 % slower on cfg2, 8 % on cfg3, same box), otherwise the quad
         // layout cbc_kernel / cbc2_kernel (4 lanes per chain)
         const char* lay_env = getenv("TLSGPU_CBC_LAYOUT");
-        const bool quad = !(lay_env && lay_env[0] == 'p') || ilp == 2 || env_is("TLSGPU_CBC_IO", '1');
+        const bool quad = (!(lay_env && lay_env[0] == 'p') || ilp == 2 || env_is("TLSGPU_CBC_IO", '1')) &&
+                          (nchains + ncu - 1) / ncu <= (uint32_t)C3_CHAINS;  // > 256 chains per CU: pair layout
         if (!quad) {
-            uint32_t pw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
+            uint32_t pw = (nchains + ncu - 1) / ncu;
             pw = pw < 1 ? 1 : (pw > (uint32_t)CP_CHAINS ? (uint32_t)CP_CHAINS : pw);
             auto kern = cbcp_kernel<NR>;
             static bool attrp = false;
@@ -563,7 +566,7 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
                                recs, nrecords, pt, wire, states, meta, tails, pw, epoch, debug_skip_flags());
             return hipGetLastError();
         }
-        uint32_t cpw = (nchains + cu_count() - 1) / (uint32_t)cu_count();
+        uint32_t cpw = (nchains + ncu - 1) / ncu;
         cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
         if (ilp == 2) {
             auto kern = cbc2_kernel<NR>;
@@ -606,7 +609,7 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
                               const tlsgpu_record* recs, uint32_t nrecords, const uint8_t* pt, uint8_t* wire,
                               ConnState* states, int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s1,
                               hipEvent_t mac_done, hipStream_t s2, hipEvent_t cbc_start, hipEvent_t cbc_stop,
-                              bool* known) {
+                              bool* known, int cbc_cus) {
     *known = true;
     hipError_t e = hipSuccess;
 #define TG_PH(CID, NR, MAC_ID, SSL3)                                                                            \
@@ -617,7 +620,7 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
         if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                          \
         if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                                   \
         if (cbc_start && (e = hipEventRecord(cbc_start, s2)) != hipSuccess) return e;                           \
-        e = launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s2);              \
+        e = launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s2, cbc_cus);     \
         if (e == hipSuccess && cbc_stop) e = hipEventRecord(cbc_stop, s2);                                       \
         return e;                                                                                                \
     }
