@@ -550,8 +550,10 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         // chains per CU; A/B only: 5 % slower on cfg2, 8 % on cfg3, same box), otherwise the quad
         // layout cbc_kernel / cbc2_kernel (4 lanes per chain)
         const char* lay_env = getenv("TLSGPU_CBC_LAYOUT");
+        // on a CU-masked stream (cus > 0) more than 256 chains per CU need the pair layout (one
+        // workgroup generation); on the whole chip extra chains run as further generations
         const bool quad = (!(lay_env && lay_env[0] == 'p') || ilp == 2 || env_is("TLSGPU_CBC_IO", '1')) &&
-                          (nchains + ncu - 1) / ncu <= (uint32_t)C3_CHAINS;  // > 256 chains per CU: pair layout
+                          (cus <= 0 || (nchains + ncu - 1) / ncu <= (uint32_t)C3_CHAINS);
         if (!quad) {
             uint32_t pw = (nchains + ncu - 1) / ncu;
             pw = pw < 1 ? 1 : (pw > (uint32_t)CP_CHAINS ? (uint32_t)CP_CHAINS : pw);
@@ -588,8 +590,11 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
             if (e != hipSuccess) return e;
             attr[io16] = true;
         }
-        hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C3_THREADS), AES_LDS_BYTES, s, chains, nchains, recs,
-                           nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
+        // persistent: at most one workgroup per CU, quads loop over chain generations
+        uint32_t grid = (nchains + cpw - 1) / cpw;
+        grid = grid > ncu ? ncu : grid;
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(C3_THREADS), AES_LDS_BYTES, s, chains, nchains, recs, nrecords, pt,
+                           wire, states, meta, tails, cpw, epoch, debug_skip_flags());
         return hipGetLastError();
     }
 }
