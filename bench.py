@@ -51,6 +51,37 @@ def parse():
     return ap.parse_args()
 
 
+# The reference's own pure-Python path (measured in the survey container through
+# the namespace shim: TLSRecordLayer._sendMsg with the "python" cipher implementation, 16 KiB
+# AES-128-CBC + HMAC-SHA1 records, TLS 1.2).  It cannot run on the GPU box (the reference does
+# not travel), so it is quoted, labelled, beside the measured C-restatement baseline.
+REFERENCE_PYTHON = {"value": round(4.03e6 / GIB, 6), "unit": "GiB/s", "cores": 8, "per_core": round(0.621e6 / GIB, 6),
+                    "kind": "reference",
+                    "where": "survey container, Intel Xeon 8 cores (multiprocessing.Pool(8)); BASELINE.md",
+                    "what": "tlslite 0.4.9 TLSRecordLayer._sendMsg, pure-Python AES-128-CBC + HMAC-SHA1 (stdlib "
+                            "hmac), 16 KiB records, TLS 1.2"}
+
+
+def usable_cpus():
+    """Host cores this job may use: the affinity mask, capped by a cgroup CPU quota and by
+    OMP_NUM_THREADS (the GPU box sets it to the CPU share of one GPU); -> (threads, note)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    note = ["affinity %d" % n, "os.cpu_count %d" % (os.cpu_count() or 0)]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            lim = max(1, int(int(q) // int(per)))
+            note.append("cgroup quota %d" % lim)
+            n = min(n, lim)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        note.append("OMP_NUM_THREADS %s" % omp)
+        n = min(n, int(omp))
+    return n, ", ".join(note)
+
+
 def build_workload(name, rank, world, records=None):
     from tlslite_amd import workloads as W
     if name == "cfg4":
@@ -263,15 +294,18 @@ def main():
         wl.launch([stream])
         stream.synchronize()
         wire_gpu = wl.d_wire.download()
-        nthreads = min(16, os.cpu_count() or 1)
+        nthreads, cpu_note = usable_cpus()
         ok, dt, nrec, ptb, th, reps = oracle_check(wl, wire_gpu, nthreads,
                                                    min_seconds=0.0 if args.no_cpu else args.cpu_seconds)
         bit_exact = ok
         if not args.no_cpu:
-            cpu = {"value": round(ptb / GIB / dt, 4), "unit": "GiB/s", "cores": th, "kind": "port",
+            cpu = {"value": round(ptb / GIB / dt, 4), "unit": "GiB/s", "cores": th,
+                   "per_core": round(ptb / GIB / dt / th, 5), "kind": "port",
                    "sample": "full batch (%d records, %.1f MiB plaintext) sealed %d times in succession by "
                              "oracle/tls_oracle.c (C restatement of tlslite's _sendMsg path), %d pthreads, %.2f s"
-                             % (nrec, ptb / reps / 2 ** 20, reps, th, dt)}
+                             % (nrec, ptb / reps / 2 ** 20, reps, th, dt),
+                   "cores_note": "threads = the host cores this job may use (%s)" % cpu_note,
+                   "reference_python": REFERENCE_PYTHON}
         wl.reset_states(stream)
         stream.synchronize()
 

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define TLSGPU_ABI_VERSION 1
+#define TLSGPU_ABI_VERSION 2
 
 /* ---- suite components (tlsrecordlayer.py:1063-1095, constants.py:159-201) */
 enum {
@@ -72,7 +72,11 @@ enum {
     TLSGPU_EMISMATCH = -5,  /* connection state does not match the launch variant */
     /* open-path per-record status (alerts, tlsrecordlayer.py:964-1042) */
     TLSGPU_ALERT_BAD_RECORD_MAC = -20,
-    TLSGPU_ALERT_DECRYPTION_FAILED = -21
+    TLSGPU_ALERT_DECRYPTION_FAILED = -21,
+    /* open with TLSGPU_CHAIN_STOP_ON_ALERT: not opened, an earlier record of the
+     * chain raised an alert (the reference sends the alert and closes the
+     * connection there: tlsrecordlayer.py:1039-1042 -> _sendError) */
+    TLSGPU_ALERT_SKIPPED = -22
 };
 
 /* Launch variant = one (cipher, MAC, SSL3-or-TLS) kernel instantiation.
@@ -101,14 +105,19 @@ typedef struct tlsgpu_record {
     uint16_t reserved;
 } tlsgpu_record;
 
-/* A run of records of ONE connection, sealed in order (CBC residue, RC4
- * keystream and seqnum carried from record to record).  Independent chains
- * run in parallel; a record must belong to exactly one chain. */
+/* A run of records of ONE connection, sealed (or opened) in order (CBC
+ * residue, RC4 keystream and seqnum carried from record to record).
+ * Independent chains run in parallel; a record must belong to exactly one
+ * chain. */
+#define TLSGPU_CHAIN_STOP_ON_ALERT 1u /* open: records after the first alert are not
+                                         opened (status TLSGPU_ALERT_SKIPPED) and the
+                                         state stays as the failing record left it */
 typedef struct tlsgpu_chain {
     uint32_t state;    /* index into the states array */
     uint32_t first;    /* first record index */
     uint32_t count;    /* number of records */
-    uint32_t reserved;
+    uint32_t flags;    /* TLSGPU_CHAIN_* (0: every record opened, as successive
+                          _decryptRecord calls; seal ignores it) */
 } tlsgpu_chain;
 
 /* One record to open.  Body (ciphertext, header already parsed) at
@@ -207,10 +216,10 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state *st, uint32_t pt_len, uint32_t 
  * for an empty record, or a negative TLSGPU_E* code.  All chains of one
  * launch must use connection states of `variant`; `records` has `nrecords`
  * entries (chains index into it). */
-/* Device workspace for a seal of `nrecords` descriptors (AES suites: per
- * record 32 B of metadata + a 64 B CBC-tail slot).  Pass it to
- * tlsgpu_seal_dev, or pass NULL there to use a library-owned per-device
- * workspace (then calls on different streams must not overlap). */
+/* Device workspace for a seal of `nrecords` descriptors (AES / 3DES suites:
+ * per record 32 B of metadata + a 64 B CBC-tail slot).  Pass it to
+ * tlsgpu_seal_dev, or pass NULL there to use a library-owned workspace, one
+ * per (device, stream): calls on different streams never share one. */
 size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords);
 int tlsgpu_seal_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_record *records,
                     uint32_t nrecords, const uint8_t *pt, uint8_t *wire, tlsgpu_conn_state *states,
@@ -232,6 +241,8 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain *chains, uint32_t
 
 /* Batch open: status[r] = plaintext length, or TLSGPU_ALERT_* (records 0..nrecords-1;
  * a chain's records open in order on its state, as successive _decryptRecord calls).
+ * A connection must not accept records after an alert: set TLSGPU_CHAIN_STOP_ON_ALERT
+ * on its chain (or stop at the first negative status yourself).
  * The whole decrypted body after the explicit IV (payload | MAC | padding, ct_len - IV
  * bytes) is written at pt + pt_off: size the plaintext slots for it.
  * AES suites decrypt every block of every record in parallel and need a workspace of

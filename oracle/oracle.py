@@ -201,9 +201,11 @@ def fill_pattern(n, seed, start=0):
     return a
 
 
-def seal_batch(protos, chain_begin, chain_count, pt, pt_off, pt_len, wire, wire_off, ctype=None, nthreads=1):
+def seal_batch(protos, chain_begin, chain_count, pt, pt_off, pt_len, wire, wire_off, ctype=None, nthreads=1,
+               update=False):
     """Seal many chains in parallel threads.  protos: list of Conn (one per
-    chain, copied -- the originals are not advanced).  Returns wire_len array."""
+    chain, copied -- the originals are advanced only with update=True).
+    Returns wire_len array."""
     L = lib()
     sz = L.ora_conn_size()
     arr = ctypes.create_string_buffer(sz * len(protos))
@@ -219,4 +221,7 @@ def seal_batch(protos, chain_begin, chain_count, pt, pt_off, pt_len, wire, wire_
     L.ora_seal_batch(arr, len(protos), chain_begin.ctypes.data, chain_count.ctypes.data, pt.ctypes.data,
                      pt_off.ctypes.data, pt_len.ctypes.data, None if ct is None else ct.ctypes.data,
                      wire.ctypes.data, wire_off.ctypes.data, wl.ctypes.data, nthreads)
+    if update:
+        for i, c in enumerate(protos):
+            ctypes.memmove(c.buf, ctypes.addressof(arr) + i * sz, sz)
     return wl

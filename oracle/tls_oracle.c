@@ -645,7 +645,7 @@ size_t ora_conn_size(void) { return sizeof(ora_conn); }
  * Threads split the independent chains.  Used only for cpu_baseline and for
  * full-size parity digests.                                                  */
 typedef struct {
-    const ora_conn *protos;   /* one per chain */
+    ora_conn *protos;   /* one per chain */
     const uint8_t *pt;        /* plaintext arena */
     const uint64_t *pt_off; const uint32_t *pt_len; const uint64_t *wire_off;
     const uint8_t *ctype;
@@ -664,11 +664,12 @@ static void *batch_worker(void *p) {
             a->wire_len[r] = ora_seal(&c, a->ctype ? a->ctype[r] : 23, a->pt + a->pt_off[r], a->pt_len[r], 0,
                                       a->wire + a->wire_off[r], (size_t)1 << 20);
         }
+        a->protos[ch] = c; /* the chain's state after its records (residue, RC4, seqnum) */
     }
     return NULL;
 }
 
-int ora_seal_batch(const ora_conn *protos, size_t nchains, const uint32_t *chain_begin, const uint32_t *chain_count,
+int ora_seal_batch(ora_conn *protos, size_t nchains, const uint32_t *chain_begin, const uint32_t *chain_count,
                    const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len, const uint8_t *ctype,
                    uint8_t *wire, const uint64_t *wire_off, long *wire_len, int nthreads) {
     if (nthreads < 1) nthreads = 1;

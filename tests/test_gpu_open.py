@@ -160,7 +160,7 @@ def test_malformed_chains_like_oracle(suite, version):
             else:
                 body = w_o.seal(rng.bytes(int(rng.integers(1, 200))), 23)[5:]
             recs.append((ci, 23, body))
-    res = open_records(readers, recs)
+    res = open_records(readers, recs, stop_on_alert=False)
     amap = {0: 0, O.ALERT_BAD_RECORD_MAC: N.ALERT_BAD_RECORD_MAC,
             O.ALERT_DECRYPTION_FAILED: N.ALERT_DECRYPTION_FAILED}
     for (ci, ct, body), (st, p) in zip(recs, res):
@@ -176,14 +176,12 @@ def test_malformed_chains_like_oracle(suite, version):
             assert r.iv == o.iv
 
 
-@pytest.mark.parametrize("impl", ["split", "lane"])
-def test_golden_open_chains(golden, impl, monkeypatch):
+def test_golden_open_chains(golden):
     """The reference's _decryptRecord statuses / plaintexts / final state over
-    chains of valid, tampered and malformed bodies (tests/golden open cases),
-    all chains in one open_records call per variant; AES through the
-    block-parallel path (split) and the one-lane-per-chain kernel (lane)."""
+    chains of valid, tampered and malformed bodies (tests/golden open cases:
+    successive _decryptRecord calls that continue after an alert), all chains in
+    one open_records call per variant, without stop-on-alert."""
     from tlslite_amd import _native as N
-    monkeypatch.setenv("TLSGPU_OPEN_IMPL", impl)
     from tlslite_amd.recordlayer import open_records
     T = _T()
     amap = {0: 0, 20: N.ALERT_BAD_RECORD_MAC, 21: N.ALERT_DECRYPTION_FAILED}
@@ -199,7 +197,7 @@ def test_golden_open_chains(golden, impl, monkeypatch):
             recs.append((si, b["type"], bytes.fromhex(b["body"])))
             expect.append((amap[b["status"]], bytes.fromhex(b["pt"]) if b["status"] == 0 else None))
     assert len(cases) == 22
-    res = open_records(states, recs)
+    res = open_records(states, recs, stop_on_alert=False)
     for (st, pt), (est, ept) in zip(res, expect):
         assert st == est
         if est == 0:
@@ -212,3 +210,62 @@ def test_golden_open_chains(golden, impl, monkeypatch):
         else:
             S, i, j = s.rc4
             assert (S.hex(), i, j) == (f["rc4_S"], f["rc4_i"], f["rc4_j"]), c["name"]
+
+
+@pytest.mark.parametrize("suite", ["AES128-SHA", "AES256-SHA256", "3DES-SHA", "RC4-SHA"])
+@pytest.mark.parametrize("version", [(3, 0), (3, 1), (3, 3)])
+def test_stop_on_alert_like_connection(suite, version):
+    """Connection semantics (the default of open_records): a chain stops at its
+    first alert -- the reference's _getMsg raises and _sendError closes the
+    connection (tlsrecordlayer.py:1039-1042) -- so no plaintext after a tampered
+    or dropped record is returned (ALERT_SKIPPED), and the state is the one the
+    failing record left, equal to the oracle's after opening records up to and
+    including the failing one."""
+    from oracle import oracle as O
+    from tlslite_amd import _native as N
+    from tlslite_amd.recordlayer import open_records
+    T = _T()
+    if suite.endswith("SHA256") and version != (3, 3):
+        pytest.skip("TLS 1.2 only")
+    rng = np.random.default_rng(zlib.crc32(repr(("stop", suite, version)).encode()))
+    amap = {0: 0, O.ALERT_BAD_RECORD_MAC: N.ALERT_BAD_RECORD_MAC,
+            O.ALERT_DECRYPTION_FAILED: N.ALERT_DECRYPTION_FAILED}
+    readers, oreaders, recs, fail_at = [], [], [], []
+    for ci in range(40):
+        mk_t, mk_o = _mk(T, O, suite, version, rng)
+        w_t = mk_t()
+        readers.append(mk_t())
+        oreaders.append(mk_o())
+        n = int(rng.integers(3, 7))
+        bad = int(rng.integers(0, n + 1)) if ci % 4 else n  # every 4th chain clean
+        fail_at.append(bad)
+        bodies = [w[5:] for w in T.seal([w_t], [(0, rng.bytes(int(rng.integers(1, 300))))
+                                                for _ in range(n)])]
+        for k, b in enumerate(bodies):
+            if k == bad:
+                b = bytearray(b)
+                if ci % 3 == 0 and O.SUITES[suite][0] != "rc4":
+                    b = b[:-1]  # decryption_failed
+                else:
+                    b[int(rng.integers(0, len(b)))] ^= 0x10
+                b = bytes(b)
+            recs.append((ci, 23, b))
+    res = open_records(readers, recs)
+    k_of = {}
+    for (ci, ct, body), (st, p) in zip(recs, res):
+        k = k_of.get(ci, 0)
+        k_of[ci] = k + 1
+        if k < fail_at[ci]:
+            ost, opt = oreaders[ci].open(body, ct)
+            assert (st, p) == (0, opt) and ost == 0
+        elif k == fail_at[ci]:
+            ost, _ = oreaders[ci].open(body, ct)
+            assert ost < 0 and st == amap[ost] and p is None
+        else:
+            assert st == N.ALERT_SKIPPED and p is None
+    for r, o in zip(readers, oreaders):
+        assert r.seqnum == o.seqnum
+        if O.SUITES[suite][0] == "rc4":
+            assert r.rc4 == o.rc4
+        else:
+            assert r.iv == o.iv

@@ -100,28 +100,41 @@ def test_random_lengths_vs_oracle(suite, version):
         assert w == ocs[ci].seal(p, ct, fl), (suite, version, len(p), fl)
 
 
-def _mixed_workload(n, pt_len, seed):
+def _mixed_workload(n, pt_len, seed, suites=("AES128-SHA", "RC4-SHA")):
+    """Two suites, 3 chained records per connection, records of both suites
+    interleaved in the arenas (seeded shuffle)."""
     from tlslite_amd import workloads as W
+    from oracle import oracle as O
     rng = np.random.default_rng(seed)
     h = n // 2
-    ka, mka, fiva = rng.bytes(16), rng.bytes(20), rng.bytes(16)
-    kr, mkr = rng.bytes(16), rng.bytes(20)
-    iva = np.frombuffer(rng.bytes(16 * h), dtype=np.uint8).reshape(h, 16)
-    g1 = W.Group("AES128-SHA", (3, 3), [ka], iva, [mka], [fiva], np.arange(h, dtype=np.uint64), 3, pt_len)
-    g2 = W.Group("RC4-SHA", (3, 1), [kr], None, [mkr], None, np.arange(n - h, dtype=np.uint64), 3, pt_len)
-    return W.Workload("mixed", [g1, g2], seed, rec_order=rng.permutation(3 * n))
+    groups = []
+    for suite, nconn, version in ((suites[0], h, (3, 3)), (suites[1], n - h, (3, 1))):
+        _, kl, ivl, _, ml = O.SUITES[suite]
+        key, mk = rng.bytes(kl), rng.bytes(ml)
+        fiv = [rng.bytes(ivl)] if ivl else None
+        ivs = np.frombuffer(rng.bytes(ivl * nconn), dtype=np.uint8).reshape(nconn, ivl) if ivl else None
+        groups.append(W.Group(suite, version, [key], ivs, [mk], fiv, np.arange(nconn, dtype=np.uint64), 3, pt_len))
+    return W.Workload("mixed", groups, seed, rec_order=rng.permutation(3 * n))
 
 
-@pytest.mark.parametrize("kind", ["cfg2", "mixed"])
+@pytest.mark.parametrize("kind", ["cfg2", "mixed", "3des", "rc4_3des"])
 def test_pipeline_equals_sequential(kind):
     """tlsgpu_pipeline_seal: K successive batches (MAC phase of batch k+1
-    overlapping the CBC phase of batch k) give the same wire bytes and final
-    connection states as K sequential tlsgpu_seal_dev calls."""
+    overlapping the cipher phase of batch k) give the same wire bytes and final
+    connection states as K sequential tlsgpu_seal_dev calls -- for AES, the
+    3DES split path (prefix / MAC / tdes8_kernel) and RC4 + 3DES mixes."""
     _T()
     from tlslite_amd import workloads as W
     from tlslite_amd.device import DeviceBuffer, Stream
     from tlslite_amd.recordlayer import SealPipeline
-    wl = W.cfg2(n=700, pt_len=5003, seed=11) if kind == "cfg2" else _mixed_workload(300, 2000, 12)
+    if kind == "cfg2":
+        wl = W.cfg2(n=700, pt_len=5003, seed=11)
+    elif kind == "mixed":
+        wl = _mixed_workload(300, 2000, 12)
+    elif kind == "3des":
+        wl = _mixed_workload(300, 2003, 13, ("3DES-SHA", "3DES-SHA"))
+    else:
+        wl = _mixed_workload(300, 1999, 14, ("3DES-SHA", "RC4-SHA"))
     wl.to_device()
     K = 4
     s = Stream()
@@ -162,33 +175,24 @@ def test_pipeline_equals_sequential(kind):
     assert pipe_states == seq_states
     # successive batches really chain: a later batch differs from the first
     assert seq_out[1][0] != seq_out[0][0]
+    # and the first batch is the oracle's
+    from tests.wl_oracle import oracle_seal
+    wl.reset_states(s)
+    s.synchronize()
+    wire, lens, _ = oracle_seal(wl)
+    assert np.frombuffer(seq_out[0][1], dtype=np.int32).tolist() == lens.tolist()
+    assert seq_out[0][0] == wire.tobytes()
     wl.free()
 
 
-# AES seal kernel selections (environment switches read per launch by libtlsgpu)
-AES_IMPLS = {
-    "cbc1": {},                                   # default: cbc_kernel, column-word I/O, per-lane MAC loads
-    "cbc1io16": {"TLSGPU_CBC_IO": "16"},          # cbc_kernel<NR, IO16>: 16-byte I/O + quad transposes
-    "macquad": {"TLSGPU_MAC_LOAD": "quad"},       # mac_kernel<.., QL>: quad-cooperative loads
-    "cbc2": {"TLSGPU_CBC_ILP": "2"},              # cbc2_kernel: two chains per quad
-    "pair": {"TLSGPU_CBC_LAYOUT": "pair"},        # cbcp_kernel: two lanes per chain
-    "fused": {"TLSGPU_SEAL_IMPL": "fused"},       # single fused quad kernel
-    "lane": {"TLSGPU_SEAL_IMPL": "lane"},         # one lane per chain
-}
-
-
-@pytest.mark.parametrize("ilp", list(AES_IMPLS))
-@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 1)), ("AES256-SHA256", (3, 3)), ("AES128-SHA", (3, 0))])
-def test_cbc_variants_chained_vs_oracle(ilp, suite, version, monkeypatch):
-    """Every AES seal kernel -- split path with cbc_kernel (one chain per quad;
-    column-word or 16-byte I/O; per-lane or quad-cooperative MAC loads) or
-    cbc2_kernel (two chains per quad, bulk interleaved, IV/tail blocks one chain
-    at a time), the fused single-kernel path, the 1-lane kernel -- on chains of
-    mixed record counts and lengths (incl. empty and sub-block records) equals
-    the oracle, including the final CBC residue and seqnum."""
+@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 1)), ("AES256-SHA256", (3, 3)), ("AES128-SHA", (3, 0)),
+                                           ("3DES-SHA", (3, 2))])
+def test_chained_vs_oracle(suite, version):
+    """The split seal path (seqnum prefix, per-record MAC, quad-lane CBC or
+    8-lane 3DES) on chains of mixed record counts and lengths (incl. empty and
+    sub-block records) equals the oracle, including the final CBC residue and
+    seqnum."""
     from oracle import oracle as O
-    for k, v in AES_IMPLS[ilp].items():
-        monkeypatch.setenv(k, v)
     T = _T()
     rng = np.random.default_rng(zlib.crc32(repr(("ilp", suite, version)).encode()))
     cipher, kl, ivl, mac, ml = O.SUITES[suite]
@@ -199,30 +203,61 @@ def test_cbc_variants_chained_vs_oracle(ilp, suite, version, monkeypatch):
         states.append(T.ConnectionState.for_suite(suite, version, key, iv, mk, fiv, seq))
         ocs.append(O.Conn.for_suite(suite, version, key, iv, mk, fiv, seq))
         for _ in range(int(rng.integers(0, 6))):
-            n = int(rng.choice([0, 1, 15, 16, 17, 100, 1434, 4000, 16384]))
+            n = int(rng.choice([0, 1, 7, 8, 15, 16, 17, 100, 1434, 4000, 16384]))
             recs.append((ci, rng.bytes(n), 23, 0))
     out = T.seal(states, recs)
     for (ci, p, ct, fl), w in zip(recs, out):
-        assert w == ocs[ci].seal(p, ct, fl), (ilp, suite, version, len(p))
+        assert w == ocs[ci].seal(p, ct, fl), (suite, version, len(p))
     for s, o in zip(states, ocs):
         assert s.seqnum == o.seqnum and s.iv == o.iv
 
 
-@pytest.mark.parametrize("impl", ["cbc1", "cbc1io16", "macquad"])
+def test_persistent_generations_vs_oracle():
+    """More chains in one launch than CUs x 256: cbc_kernel's quads take a
+    second chain generation (cid += gridDim.x * cpw).  71,000 AES256-SHA256
+    chains in ONE launch -- single records of 37 B, 3-record chains of 100 B and
+    2-record chains of 1,500 B -- plus 66,000 AES128-SHA TLS 1.1 chains; every
+    wire byte, wire length and every chain's final CBC residue and seqnum equal
+    the oracle's (python_aes.py:44, tlsrecordlayer.py:594-608)."""
+    _T()
+    from tlslite_amd import workloads as W
+    from tests.wl_oracle import device_states, oracle_seal
+    rng = np.random.default_rng(70000)
+
+    def grp(suite, version, nconn, recs, n):
+        from oracle import oracle as O
+        _, kl, ivl, _, ml = O.SUITES[suite]
+        ivs = np.frombuffer(rng.bytes(ivl * nconn), dtype=np.uint8).reshape(nconn, ivl)
+        return W.Group(suite, version, [rng.bytes(kl)], ivs, [rng.bytes(ml)], [rng.bytes(ivl)],
+                       rng.integers(0, 2 ** 40, nconn, dtype=np.uint64), recs, n)
+    groups = [grp("AES256-SHA256", (3, 3), 50000, 1, 37), grp("AES256-SHA256", (3, 3), 15000, 3, 100),
+              grp("AES256-SHA256", (3, 3), 6000, 2, 1500), grp("AES128-SHA", (3, 2), 66000, 1, 20)]
+    wl = W.Workload("generations", groups, 71, rec_order=None)
+    wl.to_device()
+    assert max(n for _, _, n in wl.launches) > 256 * 256
+    wl.launch()
+    from tlslite_amd.device import synchronize
+    synchronize()
+    wire_gpu = wl.d_wire.download()
+    lens_gpu = wl.d_len.download().view(np.int32)
+    states = device_states(wl)
+    wire, lens, conns = oracle_seal(wl, nthreads=16)
+    assert lens_gpu.tolist() == lens.tolist()
+    assert np.array_equal(wire_gpu, wire)
+    bad = [c for c, (s, o) in enumerate(zip(states, conns)) if s.iv != o.iv or s.seqnum != o.seqnum]
+    assert not bad, "chains with a wrong final state: %s" % bad[:10]
+    wl.free()
+
+
 @pytest.mark.parametrize("pt_shift,wire_shift", [(0, 0), (4, 4), (0, 4), (4, 0), (1, 0), (0, 1), (3, 7)])
-@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES128-SHA", (3, 1)), ("RC4-SHA", (3, 1))])
-def test_unaligned_arenas_vs_oracle(pt_shift, wire_shift, suite, version, impl, monkeypatch):
+@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES128-SHA", (3, 1)), ("RC4-SHA", (3, 1)),
+                                           ("3DES-SHA", (3, 3))])
+def test_unaligned_arenas_vs_oracle(pt_shift, wire_shift, suite, version):
     """Record arenas off the 16-byte grid: every record's plaintext at
     pt_off % 16 == pt_shift and its body at (wire_off + 5) % 16 == wire_shift.
-    The kernels pick 16-byte, dword or byte paths per record (and the MAC its
-    per-lane loads when a quad is not 16-byte aligned); output equals the oracle.
-    Equal-length records in runs of 4 so quad-cooperative MAC loads are taken
-    whenever the alignment allows."""
+    The kernels pick 16-byte, dword or byte paths per record; output equals the
+    oracle."""
     from oracle import oracle as O
-    if suite.startswith("RC4") and impl != "cbc1":
-        pytest.skip("AES kernel selections only")
-    for k, v in AES_IMPLS[impl].items():
-        monkeypatch.setenv(k, v)
     T = _T()
     rng = np.random.default_rng(zlib.crc32(repr(("unal", pt_shift, wire_shift, suite, version)).encode()))
     cipher, kl, ivl, mac, ml = O.SUITES[suite]

@@ -79,3 +79,102 @@ def test_two_rank_sharding_matches_single_process():
         assert merged == single
         assert t_max == 2.0
         assert total == 6 * 3 * 700
+
+
+# ---------------------------------------------------------------- HIP path, 2 ranks
+_GPU_WORKER = r'''
+import hashlib, json, os, sys
+sys.path.insert(0, os.environ["TG_ROOT"])
+import numpy as np
+from tlslite_amd import workloads as W
+from tlslite_amd.device import Stream, set_device, synchronize
+from tlslite_amd.recordlayer import SealPipeline, seal_dev
+from tlslite_amd.shard import ShardGroup, shard_indices
+g = ShardGroup("gloo")
+set_device(0)  # both ranks on the one GPU of the box: the per-device paths still run twice
+wl = W.cfg4(nconn=64, recs_per_conn=4, pt_len=3000, rank=g.rank, world=g.world)
+wl.to_device()
+synchronize()
+mine = shard_indices(64, g.rank, g.world)
+def digests():
+    wire = wl.d_wire.download()
+    out = {}
+    for c in range(wl.n_chains):
+        h = hashlib.sha256()
+        for r in range(int(wl.chain_first[c]), int(wl.chain_first[c] + wl.chain_count[c])):
+            o, L = int(wl.wire_off[r]), int(wl.wire_len[r])
+            h.update(wire[o:o + L].tobytes())
+        out[int(mine[c])] = h.hexdigest()
+    return out
+# batch 1: tlsgpu_seal_dev with the library-owned workspace, on two streams in turn
+s1, s2 = Stream(), Stream()
+var, d_ch, nch = wl.launches[0]
+seal_dev(d_ch, nch, wl.d_recs, wl.n_records, wl.d_pt, wl.d_wire, wl.d_states, wl.d_len, var, None, s1)
+s1.synchronize()
+b1 = digests()
+# batch 2: the seal pipeline (states carried from batch 1)
+pipe = SealPipeline(wl.n_records)
+wl.launch(pipeline=pipe)
+pipe.synchronize()
+pipe.close()
+b2 = digests()
+allmaps = g.gather_bytes(json.dumps([b1, b2]).encode())
+g.barrier()
+g.close()
+if g.rank == 0:
+    merged = [{}, {}]
+    for m in allmaps:
+        for k, d in enumerate(json.loads(m.decode())):
+            merged[k].update({int(a): b for a, b in d.items()})
+    print("RESULT " + json.dumps([sorted(merged[0].items()), sorted(merged[1].items())]))
+'''
+
+
+@pytest.mark.gpu
+def test_two_rank_hip_sharding_matches_oracle(tmp_path):
+    """Two processes (RANK 0/1, gloo rendezvous, both on device 0) each seal
+    their round-robin shard of 64 chained connections through libtlsgpu.so --
+    batch 1 with tlsgpu_seal_dev and the library-owned workspace, batch 2
+    through the seal pipeline with the states batch 1 left -- and the merged
+    per-connection digests equal a single-process CPU-oracle run of both
+    batches (the connection is the shard unit: tlsrecordlayer.py:27-37,
+    python_aes.py:44)."""
+    import json
+    import subprocess
+    import sys
+    from tlslite_amd import workloads as W
+    from tests.wl_oracle import oracle_seal
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "worker.py"
+    script.write_text(_GPU_WORKER)
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), TG_ROOT=root)
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=100) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-2000:]
+    line = [l for l in outs[0][0].splitlines() if l.startswith("RESULT ")][0]
+    got = [dict((int(a), b) for a, b in x) for x in json.loads(line[7:])]
+    wl = W.cfg4(nconn=64, recs_per_conn=4, pt_len=3000, rank=0, world=1)
+    wire1, _, conns = oracle_seal(wl)
+
+    def dig(wire):
+        out = {}
+        for c in range(wl.n_chains):
+            h = hashlib.sha256()
+            for r in range(int(wl.chain_first[c]), int(wl.chain_first[c] + wl.chain_count[c])):
+                o, L = int(wl.wire_off[r]), int(wl.wire_len[r])
+                h.update(wire[o:o + L].tobytes())
+            out[c] = h.hexdigest()
+        return out
+    from oracle import oracle as O
+    pt = wl.host_plaintext(O.fill_pattern)
+    wire2 = np.zeros(wl.wire_bytes, dtype=np.uint8)
+    O.seal_batch(conns, wl.chain_first, wl.chain_count, pt, wl.pt_off, wl.pt_len, wire2, wl.wire_off, nthreads=4)
+    assert got[0] == dig(wire1)
+    assert got[1] == dig(wire2)
+    assert got[0] != got[1]

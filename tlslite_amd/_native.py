@@ -15,7 +15,9 @@ CIPHER_AES128, CIPHER_AES256, CIPHER_RC4, CIPHER_3DES, CIPHER_AES192 = 1, 2, 3, 
 MAC_SHA1, MAC_SHA256, MAC_MD5 = 1, 2, 3
 FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
 OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH = 0, -1, -2, -3, -4, -5
-ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED = -20, -21
+ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED, ALERT_SKIPPED = -20, -21, -22
+CHAIN_STOP_ON_ALERT = 1
+ABI_VERSION = 2
 CONN_STATE_BYTES = 2048
 
 
@@ -30,7 +32,7 @@ class Record(ctypes.Structure):  # tlsgpu_record
 
 class Chain(ctypes.Structure):  # tlsgpu_chain
     _fields_ = [("state", ctypes.c_uint32), ("first", ctypes.c_uint32), ("count", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32)]
 
 
 class OpenRecord(ctypes.Structure):  # tlsgpu_open_record
@@ -122,6 +124,9 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if not os.environ.get("TLSGPU_LIB") and lib.tlsgpu_abi_version() != ABI_VERSION:
+        raise ImportError("libtlsgpu.so ABI %d, this binding expects %d: rebuild the library"
+                          % (lib.tlsgpu_abi_version(), ABI_VERSION))
     return lib
 
 

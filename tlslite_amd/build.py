@@ -16,7 +16,7 @@ LIB = os.path.join(LIBDIR, "libtlsgpu.so")
 ARCH = os.environ.get("TLSGPU_ARCH", "gfx950")
 
 SOURCES = ["tg_kernels.hip", "tg_api.hip"]
-HEADERS = ["tg_common.h", "tg_hash.h", "tg_device.h", "tg_aesq.h", "tg_aes3.h", "tg_open3.h", "tg_launch.h", "tg_keysched.h", "tg_derive.h"]
+HEADERS = ["tg_common.h", "tg_hash.h", "tg_device.h", "tg_quad.h", "tg_aes3.h", "tg_open3.h", "tg_launch.h", "tg_keysched.h", "tg_derive.h"]
 
 
 def _hipcc():
@@ -33,30 +33,39 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False, extra_flags=()):
-    os.makedirs(LIBDIR, exist_ok=True)
+def build(force=False, verbose=False, extra_flags=(), libdir=LIBDIR):
+    """Compile libtlsgpu.so into libdir.  extra_flags / libdir: A/B builds of the same
+    sources with a compile-time experiment switch (tools/build_ab.sh); the product is
+    the default build in tlslite_amd/lib."""
+    lib = os.path.join(libdir, "libtlsgpu.so")
+    os.makedirs(libdir, exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", "tlsgpu.h")]
-    if not force and not _stale(LIB, deps):
-        return LIB
+    if not force and not _stale(lib, deps):
+        return lib
     objs = []
     hipcc = _hipcc()
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
              "-munsafe-fp-atomics"] + list(extra_flags)
     for s in srcs:
-        o = os.path.join(LIBDIR, os.path.basename(s) + ".o")
+        o = os.path.join(libdir, os.path.basename(s) + ".o")
         cmd = [hipcc] + flags + ["-c", s, "-o", o]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
         objs.append(o)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [hipcc, "-shared", "--offload-arch=" + ARCH, "-o", tmp] + objs
     subprocess.check_call(cmd)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
-    print(LIB)
+    # python tlslite_amd/build.py [--force] [--out DIR] [-DFLAG ...]
+    args = sys.argv[1:]
+    out = LIBDIR
+    if "--out" in args:
+        out = os.path.abspath(args[args.index("--out") + 1])
+    flags = [a for a in args if a.startswith("-D")]
+    print(build(force="--force" in args or bool(flags), verbose=True, extra_flags=flags, libdir=out))

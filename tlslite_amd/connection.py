@@ -123,7 +123,8 @@ def derive_pending_states_gpu(conns, premaster=False, want_key_block=False, stre
     at once on the GPU.  conns: iterable of dicts with `secret` (48-byte
     master secret, or premaster when premaster=True: calcMasterSecret
     mathtls.py:70-82 runs first), `client_random`, `server_random`, `suite`,
-    `version`, `client` (bool) and optional `fixed_iv`.  Raises ValueError
+    `version`, `client` (bool) and optional `fixed_iv` (random when absent,
+    as the reference's getRandomBytes).  Raises ValueError
     (the reference's AssertionError paths) if any connection has an
     unknown suite or version."""
     from .device import DeviceBuffer, synchronize
@@ -138,7 +139,8 @@ def derive_pending_states_gpu(conns, premaster=False, want_key_block=False, stre
             if len(v) != size:
                 raise ValueError("%s must be %d bytes" % (field, size))
             ctypes.memmove(ctypes.addressof(d) + getattr(N.DeriveDesc, field).offset, v, size)
-        fiv = bytes(c.get("fixed_iv") or b"")[:16]
+        # the sender's fixedIVBlock is getRandomBytes(ivLength) (tlsrecordlayer.py:1146-1149)
+        fiv = bytes(c.get("fixed_iv") or os.urandom(16))[:16]
         ctypes.memmove(ctypes.addressof(d) + N.DeriveDesc.fixed_iv.offset, fiv, len(fiv))
         suite = c["suite"]
         d.suite = SUITE_NAMES[suite] if isinstance(suite, str) else int(suite)
@@ -203,7 +205,9 @@ class RecordLayer:
                 if ct == ContentType.application_data:
                     self._plain += p
                 elif ct == ContentType.alert:
-                    self.closed = True
+                    self.closed = True  # nothing after an alert is delivered
+                    self._inbuf = b""
+                    break
         return True
 
     def read(self, max=None, min=1):

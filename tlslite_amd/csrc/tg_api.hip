@@ -5,6 +5,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <stdio.h>
+#include <map>
+#include <mutex>
 #include "tg_common.h"
 #include "tg_hash.h"
 #include "tg_keysched.h"
@@ -237,22 +239,37 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state* st, uint32_t pt_len, uint32_t*
 
 size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords) { return seal_workspace_bytes(nrecords); }
 
-// library-owned workspace: per device and per kind, grow-only (calls that use it must not
-// run concurrently on several streams: pass a workspace for that)
-static int own_workspace(int kind, size_t need, uint8_t** out) {
-    static thread_local void* own[2][64] = {{nullptr}};
-    static thread_local size_t own_bytes[2][64] = {{0}};
+// library-owned workspace: one grow-only buffer per (kind, device, stream), so calls
+// on different streams never share one and calls on one stream are ordered by it
+static int own_workspace(int kind, size_t need, hipStream_t stream, uint8_t** out) {
+    struct Key {
+        int kind, dev;
+        hipStream_t s;
+        bool operator<(const Key& o) const {
+            return kind != o.kind ? kind < o.kind : dev != o.dev ? dev < o.dev : s < o.s;
+        }
+    };
+    struct Buf {
+        void* p = nullptr;
+        size_t bytes = 0;
+    };
+    static std::mutex mu;
+    static std::map<Key, Buf> own;
     int dev = 0;
-    (void)hipGetDevice(&dev);
-    dev &= 63;
-    if (own_bytes[kind][dev] < need) {
-        if (own[kind][dev]) TG_HIP(hipFree(own[kind][dev]));
-        own[kind][dev] = nullptr;
-        own_bytes[kind][dev] = 0;
-        TG_HIP(hipMalloc(&own[kind][dev], need));
-        own_bytes[kind][dev] = need;
+    TG_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(mu);
+    Buf& b = own[Key{kind, dev, stream}];
+    if (b.bytes < need) {
+        if (b.p) {
+            TG_HIP(hipStreamSynchronize(stream));  // earlier calls on this stream may still read it
+            TG_HIP(hipFree(b.p));
+        }
+        b.p = nullptr;
+        b.bytes = 0;
+        TG_HIP(hipMalloc(&b.p, need));
+        b.bytes = need;
     }
-    *out = static_cast<uint8_t*>(own[kind][dev]);
+    *out = static_cast<uint8_t*>(b.p);
     return 0;
 }
 
@@ -271,7 +288,7 @@ int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_r
         const size_t need = seal_workspace_bytes(nrecords);
         if (ws && workspace_bytes < need) return fail(TLSGPU_EINVAL, "workspace too small");
         if (!ws) {
-            int rc = own_workspace(0, need, &ws);
+            int rc = own_workspace(0, need, HS(s), &ws);
             if (rc) return rc;
         }
     }
@@ -287,7 +304,6 @@ int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_r
 struct tlsgpu_pipeline_s {
     int dev;
     hipStream_t mac_s, cbc_s;
-    int cbc_cus;  // CUs of the cipher stream's mask (0 = all)
     hipEvent_t mac_done[2], cbc_done[2];
     void* ws[2];
     size_t ws_bytes;
@@ -298,29 +314,8 @@ int tlsgpu_pipeline_create(tlsgpu_pipeline* out, uint32_t max_records) {
     if (!out) return fail(TLSGPU_EINVAL, "null");
     tlsgpu_pipeline p = new tlsgpu_pipeline_s();
     TG_HIP(hipGetDevice(&p->dev));
-    // TLSGPU_PIPE_MAC_CUS=N (experiment): the MAC phase on N CUs, the cipher phase on the rest
-    // (CU-masked streams, every k-th CU to the MAC side) instead of both sharing every CU
-    int ncu = 0;
-    TG_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, p->dev));
-    const char* mc = getenv("TLSGPU_PIPE_MAC_CUS");
-    const int nmac = mc ? atoi(mc) : 0;
-    p->cbc_cus = 0;
-    if (nmac > 0 && nmac < ncu && ncu <= 1024) {
-        uint32_t mmask[32] = {0}, cmask[32] = {0};
-        const int words = (ncu + 31) / 32;
-        int taken = 0;
-        for (int i = 0; i < ncu; i++) {
-            const bool mac = taken < nmac && (long)i * nmac / ncu != (long)(i + 1) * nmac / ncu;
-            if (mac) taken++;
-            (mac ? mmask : cmask)[i / 32] |= 1u << (i % 32);
-        }
-        TG_HIP(hipExtStreamCreateWithCUMask(&p->mac_s, (uint32_t)words, mmask));
-        TG_HIP(hipExtStreamCreateWithCUMask(&p->cbc_s, (uint32_t)words, cmask));
-        p->cbc_cus = ncu - taken;
-    } else {
-        TG_HIP(hipStreamCreateWithFlags(&p->mac_s, hipStreamNonBlocking));
-        TG_HIP(hipStreamCreateWithFlags(&p->cbc_s, hipStreamNonBlocking));
-    }
+    TG_HIP(hipStreamCreateWithFlags(&p->mac_s, hipStreamNonBlocking));
+    TG_HIP(hipStreamCreateWithFlags(&p->cbc_s, hipStreamNonBlocking));
     for (int i = 0; i < 2; i++) {
         TG_HIP(hipEventCreateWithFlags(&p->mac_done[i], hipEventDisableTiming));
         TG_HIP(hipEventCreateWithFlags(&p->cbc_done[i], hipEventDisableTiming));
@@ -372,7 +367,7 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain* chains, uint32_t
         e = launch_seal_phases(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len,
                                static_cast<uint8_t*>(p->ws[i]), epoch, p->mac_s, p->mac_done[i], p->cbc_s,
                                reinterpret_cast<hipEvent_t>(cipher_start), reinterpret_cast<hipEvent_t>(cipher_stop),
-                               &known, p->cbc_cus);
+                               &known);
     } else {
         // single-kernel variants run on the cipher stream, in order with earlier calls
         if (cipher_start) TG_HIP(hipEventRecord(reinterpret_cast<hipEvent_t>(cipher_start), p->cbc_s));
@@ -410,7 +405,7 @@ int tlsgpu_open_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_o
         const size_t need = open_workspace_bytes(nrecords);
         if (ws && workspace_bytes < need) return fail(TLSGPU_EINVAL, "workspace too small");
         if (!ws) {
-            int rc = own_workspace(1, need, &ws);
+            int rc = own_workspace(1, need, HS(s), &ws);
             if (rc) return rc;
         }
     }

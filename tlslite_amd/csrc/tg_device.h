@@ -380,6 +380,16 @@ struct TdesCbc {
         iv[0] = d[0] = bswap32(hi);
         iv[1] = d[1] = bswap32(lo);
     }
+    // CBC decrypt (openssl_tripledes.py:40-47): p = D(c) ^ iv, iv = c
+    __device__ __forceinline__ void dec_block(uint32_t* d) {
+        const uint32_t c0 = d[0], c1 = d[1];
+        uint32_t hi = bswap32(c0), lo = bswap32(c1);
+        tdes_block<true>(hi, lo, ks, L);
+        d[0] = bswap32(hi) ^ iv[0];
+        d[1] = bswap32(lo) ^ iv[1];
+        iv[0] = c0;
+        iv[1] = c1;
+    }
     __device__ __forceinline__ void enc64(uint32_t d[16]) {
 #pragma unroll
         for (int b = 0; b < 8; b++) enc_block(d + 2 * b);

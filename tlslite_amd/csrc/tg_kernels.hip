@@ -1,13 +1,19 @@
-// tg_kernels.hip -- gfx950 kernels of libtlsgpu.so:
-//   seal_kernel    fused per-record  MAC -> pad -> CBC/RC4 encrypt -> header,
-//                  one lane per connection chain (tlsrecordlayer.py:538-617)
-//   cipher_kernel  raw stateful CBC / RC4 encrypt+decrypt for the
-//                  cipher-object surface (python_aes.py:20-69, python_rc4.py:25-41)
-//   fill_kernel    deterministic synthetic input (splitmix64 byte stream)
-#include <stdlib.h>
-#include <string.h>
+// tg_kernels.hip -- gfx950 kernels of libtlsgpu.so and their launchers:
+//   prefix/mac/cbc_kernel, tdes8_kernel   split AES / 3DES seal (tg_aes3.h)
+//   rc4_seal_kernel  fused per-record MAC -> RC4 -> header, one lane per connection
+//                    chain (tlsrecordlayer.py:538-617, python_rc4.py:25-41)
+//   open_*_kernel    AES open (tg_open3.h); open_kernel: RC4 / 3DES open, lane per chain
+//   cipher_kernel    raw stateful CBC / RC4 encrypt+decrypt for the cipher-object
+//                    surface (python_aes.py:20-69, python_rc4.py:25-41)
+//   derive_kernel    batched _calcPendingStates (tg_derive.h)
+//   fill_kernel      deterministic synthetic input (splitmix64 byte stream)
+// The library has exactly one kernel per (direction, suite variant): no runtime
+// selection between implementations.
+#include <mutex>
+#include <set>
+#include <utility>
 #include "tg_device.h"
-#include "tg_aesq.h"
+#include "tg_quad.h"
 #include "tg_aes3.h"
 #include "tg_open3.h"
 #include "tg_derive.h"
@@ -15,65 +21,32 @@
 
 namespace tg {
 
-template <class C>
-struct CipherTraits;
-template <>
-struct CipherTraits<AesCbc<10>> {
-    static constexpr int ID = TLSGPU_CIPHER_AES128;
-    static constexpr uint32_t LDS = AES_LDS_BYTES;
-};
-template <>
-struct CipherTraits<AesCbc<14>> {
-    static constexpr int ID = TLSGPU_CIPHER_AES256;
-    static constexpr uint32_t LDS = AES_LDS_BYTES;
-};
-template <>
-struct CipherTraits<TdesCbc> {
-    static constexpr int ID = TLSGPU_CIPHER_3DES;
-    static constexpr uint32_t LDS = DES_LDS_BYTES;
-};
-template <>
-struct CipherTraits<Rc4Stream> {
-    static constexpr int ID = TLSGPU_CIPHER_RC4;
-    static constexpr uint32_t LDS = RC4_LDS_BYTES_PER_WAVE * (SEAL_BLOCK / 64);
-};
+constexpr uint32_t RC4_LDS_BYTES = RC4_LDS_BYTES_PER_WAVE * (SEAL_BLOCK / 64);
 
-template <class C>
-__device__ __forceinline__ void fill_tables(uint32_t* lds) {
-    if constexpr (CipherTraits<C>::ID == TLSGPU_CIPHER_AES128 || CipherTraits<C>::ID == TLSGPU_CIPHER_AES256)
-        aes_lds_fill(lds, false);
-    else if constexpr (CipherTraits<C>::ID == TLSGPU_CIPHER_3DES)
-        des_lds_fill(lds);
-}
-
-// One lane = one chain (a connection's ordered run of records).
-template <class C, int MAC, bool SSL3>
-__global__ void __launch_bounds__(SEAL_BLOCK) seal_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
-                                                         const tlsgpu_record* __restrict__ recs,
-                                                         const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
-                                                         ConnState* __restrict__ states,
-                                                         int32_t* __restrict__ wire_len) {
+// RC4 suites: one lane = one chain (a connection's ordered run of records); the
+// keystream is serial per connection (python_rc4.py:30-35), so MAC and cipher run
+// in the same lane.
+template <int MAC, bool SSL3>
+__global__ void __launch_bounds__(SEAL_BLOCK) rc4_seal_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
+                                                             const tlsgpu_record* __restrict__ recs,
+                                                             const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
+                                                             ConnState* __restrict__ states,
+                                                             int32_t* __restrict__ wire_len) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    fill_tables<C>(lds);
-    __syncthreads();
-
     const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
     ConnState* st = states + ch.state;
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
-    constexpr int BS = C::BS;
-
-    if (st->cipher != (uint32_t)CipherTraits<C>::ID || st->mac != (uint32_t)MAC || st->ssl3 != (SSL3 ? 1u : 0u) ||
+    if (st->cipher != (uint32_t)TLSGPU_CIPHER_RC4 || st->mac != (uint32_t)MAC || st->ssl3 != (SSL3 ? 1u : 0u) ||
         st->raw) {
         for (uint32_t k = 0; k < ch.count; k++) wire_len[ch.first + k] = TLSGPU_EMISMATCH;
         return;
     }
-    C cipher;
+    Rc4Stream cipher;
     cipher.load(st, lds);
     uint64_t seq = st->seqnum;
-    const uint32_t E = (!C::STREAM && st->explicit_iv) ? (uint32_t)BS : 0u;
     const uint32_t vmaj = st->vmaj, vmin = st->vmin;
 
     for (uint32_t k = 0; k < ch.count; k++) {
@@ -83,13 +56,7 @@ __global__ void __launch_bounds__(SEAL_BLOCK) seal_kernel(const tlsgpu_chain* __
             wire_len[ch.first + k] = 0;
             continue;
         }
-        uint32_t body;
-        if (C::STREAM) {
-            body = n + DL;
-        } else {
-            uint32_t cur = E + n + DL;
-            body = cur + (BS - (cur % BS));  // pad = BS-1-(cur%BS), plus the length byte
-        }
+        const uint32_t body = n + DL;
         if (body > 0xffffu) {
             wire_len[ch.first + k] = TLSGPU_ETOOBIG;
             continue;
@@ -100,21 +67,13 @@ __global__ void __launch_bounds__(SEAL_BLOCK) seal_kernel(const tlsgpu_chain* __
 
         M mac;
         mac.begin(st, seq, R.content_type, n);
-        if (!C::STREAM && E) {  // TLS>=1.1: fixedIVBlock encrypted with the chained residue
-            uint32_t blk[4] = {st->fixed_iv[0], st->fixed_iv[1], st->fixed_iv[2], st->fixed_iv[3]};
-            if constexpr (!C::STREAM) {
-                cipher.enc_block(blk);
-                cipher.store_block(B, blk);
-            }
-        }
         const uint32_t nfull = n >> 6;
-        uint8_t* Bp = B + E;
         for (uint32_t c = 0; c < nfull; c++) {
             uint32_t cur[16];
             load64(P + 64 * c, cur);
             mac.update(cur);
             cipher.enc64(cur);
-            store64(Bp + 64 * c, cur);
+            store64(B + 64 * c, cur);
         }
         const uint32_t r = n & 63;
         uint32_t tail[16];
@@ -122,8 +81,7 @@ __global__ void __launch_bounds__(SEAL_BLOCK) seal_kernel(const tlsgpu_chain* __
         uint32_t m[8];
         mac.finish(tail, (int)r, n, st, m);
         if (R.flags & TLSGPU_FAULT_BAD_MAC) m[0] = (m[0] & ~0xffu) | ((m[0] + 1u) & 0xffu);
-
-        // tail stream = P[64*nfull ..) | MAC | pad, staged in a private buffer
+        // tail stream = P[64*nfull ..) | MAC (tlsrecordlayer.py:611-613), staged in a private buffer
         uint32_t tb[32];
 #pragma unroll
         for (int q = 0; q < 16; q++) tb[q] = tail[q];
@@ -132,23 +90,9 @@ __global__ void __launch_bounds__(SEAL_BLOCK) seal_kernel(const tlsgpu_chain* __
         uint8_t* tbb = reinterpret_cast<uint8_t*>(tb);
 #pragma unroll
         for (int i = 0; i < DL; i++) tbb[r + i] = (uint8_t)(m[i >> 2] >> (8 * (i & 3)));
-        uint8_t* Bt = Bp + 64 * nfull;
-        if constexpr (!C::STREAM) {
-            const uint32_t padl = BS - 1 - ((r + DL) % BS);
-            for (uint32_t i = 0; i <= padl; i++) tbb[r + DL + i] = (uint8_t)padl;
-            if (R.flags & TLSGPU_FAULT_BAD_PADDING) tbb[r + DL] = (uint8_t)(padl + 1);
-            const uint32_t T = r + DL + padl + 1;
-            for (uint32_t off = 0; off < T; off += BS) {
-                uint32_t blk[4];
-#pragma unroll
-                for (int q = 0; q < BS / 4; q++) blk[q] = tb[(off >> 2) + q];
-                cipher.enc_block(blk);
-                cipher.store_block(Bt + off, blk);
-            }
-        } else {
-            const uint32_t T = r + DL;
-            for (uint32_t p = 0; p < T; p++) Bt[p] = (uint8_t)(tbb[p] ^ cipher.R.ks());
-        }
+        uint8_t* Bt = B + 64 * nfull;
+        const uint32_t T = r + DL;
+        for (uint32_t p = 0; p < T; p++) Bt[p] = (uint8_t)(tbb[p] ^ cipher.R.ks());
         W[0] = R.content_type;
         W[1] = (uint8_t)vmaj;
         W[2] = (uint8_t)vmin;
@@ -234,17 +178,8 @@ __global__ void __launch_bounds__(SEAL_BLOCK) cipher_kernel(const tlsgpu_span* _
         for (uint32_t off = 0; off + 8 <= sp.len; off += 8) {
             uint32_t d[2];
             load8(src + off, d);
-            if (!DEC) {
-                c.enc_block(d);
-            } else {
-                uint32_t c0 = d[0], c1 = d[1];
-                uint32_t hi = bswap32(d[0]), lo = bswap32(d[1]);
-                tdes_block<true>(hi, lo, c.ks, c.L);
-                d[0] = bswap32(hi) ^ c.iv[0];
-                d[1] = bswap32(lo) ^ c.iv[1];
-                c.iv[0] = c0;
-                c.iv[1] = c1;
-            }
+            if (!DEC) c.enc_block(d);
+            else c.dec_block(d);
             store8(dst + off, d);
         }
         c.save(st);
@@ -256,43 +191,27 @@ __global__ void __launch_bounds__(SEAL_BLOCK) cipher_kernel(const tlsgpu_span* _
     }
 }
 
-// ---------------------------------------------------------------- record open
-// _decryptRecord (tlsrecordlayer.py:958-1044): decrypt (CBC residue / RC4
-// state carried), strip the TLS>=1.1 explicit IV, check padding, recompute and
-// compare the MAC.  One lane per chain; the plaintext (followed by the MAC
-// and padding bytes) is written at pt + pt_off.  status = plaintext length or
-// an alert code.  Two passes over the record: decrypt+store, then verify by
-// re-reading the lane's own stores.
-template <int NR>
-struct AesDecAdapter {
-    static constexpr int BS = 16;
-    AesCbcDec<NR> c;
-    __device__ __forceinline__ void load(const ConnState* st, const void* lds) { c.load(st, lds); }
-    __device__ __forceinline__ void save(ConnState* st) { c.save(st); }
-    __device__ __forceinline__ void dec_block(uint32_t* d) { c.dec_block(d); }
-};
-struct TdesDecAdapter {
-    static constexpr int BS = 8;
-    TdesCbc c;
-    __device__ __forceinline__ void load(const ConnState* st, const void* lds) { c.load(st, lds); }
-    __device__ __forceinline__ void save(ConnState* st) { c.save(st); }
-    __device__ __forceinline__ void dec_block(uint32_t* d) {
-        uint32_t c0 = d[0], c1 = d[1];
-        uint32_t hi = bswap32(d[0]), lo = bswap32(d[1]);
-        tdes_block<true>(hi, lo, c.ks, c.L);
-        d[0] = bswap32(hi) ^ c.iv[0];
-        d[1] = bswap32(lo) ^ c.iv[1];
-        c.iv[0] = c0;
-        c.iv[1] = c1;
-    }
-};
-
+// ---------------------------------------------------------------- record open (lane)
+// _decryptRecord (tlsrecordlayer.py:958-1044) for the RC4 and 3DES suites: decrypt
+// (CBC residue / RC4 state carried), strip the TLS>=1.1 explicit IV, check padding,
+// recompute and compare the MAC.  One lane per chain; the plaintext (followed by
+// the MAC and padding bytes) is written at pt + pt_off.  status = plaintext length
+// or an alert code.  With TLSGPU_CHAIN_STOP_ON_ALERT the chain stops at its first
+// alert: later records get TLSGPU_ALERT_SKIPPED and the state stays as the failing
+// record left it (the reference closes the connection there).  AES suites open on
+// the block-parallel path (tg_open3.h).
 template <int CIPHER>
-struct OpenTraits;
-template <> struct OpenTraits<TLSGPU_CIPHER_AES128> { using D = AesDecAdapter<10>; static constexpr uint32_t LDS = AES_DEC_LDS_BYTES; };
-template <> struct OpenTraits<TLSGPU_CIPHER_AES256> { using D = AesDecAdapter<14>; static constexpr uint32_t LDS = AES_DEC_LDS_BYTES; };
-template <> struct OpenTraits<TLSGPU_CIPHER_3DES> { using D = TdesDecAdapter; static constexpr uint32_t LDS = DES_LDS_BYTES; };
-template <> struct OpenTraits<TLSGPU_CIPHER_RC4> { using D = Rc4Stream; static constexpr uint32_t LDS = RC4_LDS_BYTES_PER_WAVE * (SEAL_BLOCK / 64); };
+struct OpenCipher;
+template <>
+struct OpenCipher<TLSGPU_CIPHER_3DES> {
+    using D = TdesCbc;
+    static constexpr uint32_t BS = 8, LDS = DES_LDS_BYTES;
+};
+template <>
+struct OpenCipher<TLSGPU_CIPHER_RC4> {
+    using D = Rc4Stream;
+    static constexpr uint32_t BS = 1, LDS = RC4_LDS_BYTES;
+};
 
 template <int CIPHER, int MAC, bool SSL3>
 __global__ void __launch_bounds__(SEAL_BLOCK) open_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
@@ -301,11 +220,11 @@ __global__ void __launch_bounds__(SEAL_BLOCK) open_kernel(const tlsgpu_chain* __
                                                          ConnState* __restrict__ states,
                                                          int32_t* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    constexpr bool AES = CIPHER == TLSGPU_CIPHER_AES128 || CIPHER == TLSGPU_CIPHER_AES256;
     constexpr bool STREAM = CIPHER == TLSGPU_CIPHER_RC4;
-    if constexpr (AES) aes_lds_fill(lds, true);
-    else if constexpr (CIPHER == TLSGPU_CIPHER_3DES) des_lds_fill(lds);
-    __syncthreads();
+    if constexpr (!STREAM) {
+        des_lds_fill(lds);
+        __syncthreads();
+    }
     const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
@@ -316,7 +235,8 @@ __global__ void __launch_bounds__(SEAL_BLOCK) open_kernel(const tlsgpu_chain* __
         for (uint32_t k = 0; k < ch.count; k++) status[ch.first + k] = TLSGPU_EMISMATCH;
         return;
     }
-    typename OpenTraits<CIPHER>::D dc;
+    const bool stop = (ch.flags & TLSGPU_CHAIN_STOP_ON_ALERT) != 0;
+    typename OpenCipher<CIPHER>::D dc;
     dc.load(st, lds);
     uint64_t seq = st->seqnum;
     for (uint32_t k = 0; k < ch.count; k++) {
@@ -326,25 +246,24 @@ __global__ void __launch_bounds__(SEAL_BLOCK) open_kernel(const tlsgpu_chain* __
         const uint32_t L = R.ct_len;
         uint32_t len, totalPad = 0;
         bool padGood = true;
+        int32_t res;
         if constexpr (!STREAM) {
-            constexpr uint32_t BS = OpenTraits<CIPHER>::D::BS;
+            constexpr uint32_t BS = OpenCipher<CIPHER>::BS;
             const uint32_t E = st->explicit_iv ? BS : 0u;
             if (L % BS) {  // :964-968
-                status[ch.first + k] = TLSGPU_ALERT_DECRYPTION_FAILED;
-                continue;
+                res = TLSGPU_ALERT_DECRYPTION_FAILED;
+                goto done;
             }
             for (uint32_t off = 0; off < L; off += BS) {
-                uint32_t d[4];
-                if (BS == 16) load16(Cb + off, d); else load8(Cb + off, d);
+                uint32_t d[2];
+                load8(Cb + off, d);
                 dc.dec_block(d);
-                if (off >= E) {
-                    if (BS == 16) store16(Pb + off - E, d); else store8(Pb + off - E, d);
-                }
+                if (off >= E) store8(Pb + off - E, d);
             }
             len = L > E ? L - E : 0u;  // :970-971 (b[E:] of a shorter b is empty)
-            if (len == 0) {  // :973-977
-                status[ch.first + k] = TLSGPU_ALERT_DECRYPTION_FAILED;
-                continue;
+            if (len == 0) {            // :973-977
+                res = TLSGPU_ALERT_DECRYPTION_FAILED;
+                goto done;
             }
             const uint32_t pl = Pb[len - 1];
             if (pl + 1 > len) {  // :981-983
@@ -361,75 +280,87 @@ __global__ void __launch_bounds__(SEAL_BLOCK) open_kernel(const tlsgpu_chain* __
             for (uint32_t i = 0; i < L; i++) Pb[i] = (uint8_t)(Cb[i] ^ dc.R.ks());
             len = L;
         }
-        bool macGood = true;
-        const uint32_t endLen = DL + totalPad;
-        uint32_t n = 0;
-        if (endLen > len) {  // :1006-1007
-            macGood = false;
-        } else {
-            n = len - endLen;
-            M mac;
-            mac.begin(st, seq, R.content_type, n);
-            const uint32_t nfull = n >> 6;
-            for (uint32_t c = 0; c < nfull; c++) {
-                uint32_t cur[16];
-                load64(Pb + 64 * c, cur);
-                mac.update(cur);
-            }
-            uint32_t tail[16];
-            load_partial(Pb + 64 * nfull, n & 63, tail);
-            uint32_t m[8];
-            mac.finish(tail, (int)(n & 63), n, st, m);
-            seq++;  // getSeqNumBytes (:1018) runs whenever the MAC is computed
+        {
+            bool macGood = true;
+            const uint32_t endLen = DL + totalPad;
+            uint32_t n = 0;
+            if (endLen > len) {  // :1006-1007
+                macGood = false;
+            } else {
+                n = len - endLen;
+                M mac;
+                mac.begin(st, seq, R.content_type, n);
+                const uint32_t nfull = n >> 6;
+                for (uint32_t c = 0; c < nfull; c++) {
+                    uint32_t cur[16];
+                    load64(Pb + 64 * c, cur);
+                    mac.update(cur);
+                }
+                uint32_t tail[16];
+                load_partial(Pb + 64 * nfull, n & 63, tail);
+                uint32_t m[8];
+                mac.finish(tail, (int)(n & 63), n, st, m);
+                seq++;  // getSeqNumBytes (:1018) runs whenever the MAC is computed
 #pragma unroll
-            for (int i = 0; i < DL; i++)
-                if (Pb[n + i] != (uint8_t)(m[i >> 2] >> (8 * (i & 3)))) macGood = false;
+                for (int i = 0; i < DL; i++)
+                    if (Pb[n + i] != (uint8_t)(m[i >> 2] >> (8 * (i & 3)))) macGood = false;
+            }
+            res = (padGood && macGood) ? (int32_t)n : TLSGPU_ALERT_BAD_RECORD_MAC;
         }
-        status[ch.first + k] = (padGood && macGood) ? (int32_t)n : TLSGPU_ALERT_BAD_RECORD_MAC;
+    done:
+        status[ch.first + k] = res;
+        if (stop && res < 0) {
+            for (uint32_t j = k + 1; j < ch.count; j++) status[ch.first + j] = TLSGPU_ALERT_SKIPPED;
+            break;
+        }
     }
     st->seqnum = seq;
     dc.save(st);
+}
+
+// ---------------------------------------------------------------- launch plumbing
+// hipFuncSetAttribute is per device: remember which (kernel, device) pairs have it
+static hipError_t set_lds(const void* kern, uint32_t bytes) {
+    static std::mutex mu;
+    static std::set<std::pair<const void*, int>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(mu);
+    if (done.count({kern, dev})) return hipSuccess;
+    e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) done.insert({kern, dev});
+    return e;
+}
+template <class K>
+static hipError_t set_lds(K kern, uint32_t bytes) {
+    return set_lds(reinterpret_cast<const void*>(kern), bytes);
+}
+
+// CUs of the current device (cached per device)
+static uint32_t cu_count() {
+    static int ncu[64] = {0};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    dev &= 63;
+    if (!ncu[dev]) {
+        int n = 0;
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        ncu[dev] = n > 0 ? n : 256;
+    }
+    return (uint32_t)ncu[dev];
 }
 
 template <int CIPHER, int MAC, bool SSL3>
 static hipError_t launch_open_t(const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
                                 const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s) {
     auto kern = open_kernel<CIPHER, MAC, SSL3>;
-    constexpr uint32_t lds = OpenTraits<CIPHER>::LDS;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    dim3 grid((n + SEAL_BLOCK - 1) / SEAL_BLOCK);
-    hipLaunchKernelGGL(kern, grid, dim3(SEAL_BLOCK), lds, s, chains, n, recs, wire, pt, states, status);
+    constexpr uint32_t lds = OpenCipher<CIPHER>::LDS;
+    hipError_t e = set_lds(kern, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((n + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), lds, s, chains, n, recs, wire,
+                       pt, states, status);
     return hipGetLastError();
-}
-
-static hipError_t launch_open_lane(uint32_t variant, const tlsgpu_chain* chains, uint32_t n,
-                                   const tlsgpu_open_record* recs, const uint8_t* wire, uint8_t* pt,
-                                   ConnState* states, int32_t* status, hipStream_t s, bool* known) {
-    *known = true;
-#define TG_OPEN_CASE(CIPHER_ID, MAC_ID, SSL3)                                                  \
-    if (variant == TLSGPU_VARIANT(CIPHER_ID, MAC_ID, SSL3))                                    \
-        return launch_open_t<CIPHER_ID, MAC_ID, SSL3>(chains, n, recs, wire, pt, states, status, s);
-    TG_OPEN_CASE(TLSGPU_CIPHER_AES128, TLSGPU_MAC_SHA1, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_AES256, TLSGPU_MAC_SHA1, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_AES128, TLSGPU_MAC_SHA256, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_AES256, TLSGPU_MAC_SHA256, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_3DES, TLSGPU_MAC_SHA1, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_SHA1, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_MD5, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_AES128, TLSGPU_MAC_SHA1, true)
-    TG_OPEN_CASE(TLSGPU_CIPHER_AES256, TLSGPU_MAC_SHA1, true)
-    TG_OPEN_CASE(TLSGPU_CIPHER_3DES, TLSGPU_MAC_SHA1, true)
-    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_SHA1, true)
-    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_MD5, true)
-#undef TG_OPEN_CASE
-    *known = false;
-    return hipSuccess;
 }
 
 // ---------------------------------------------------------------- synthetic input
@@ -457,54 +388,15 @@ __global__ void fill_kernel(uint8_t* __restrict__ p, size_t bytes, uint64_t seed
     }
 }
 
-// ---------------------------------------------------------------- launchers
-template <class K>
-static hipError_t set_lds(K kern, uint32_t bytes) {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)bytes);
-}
-
-// AES implementation: 0 = split (prefix/mac/cbc, default), 1 = fused quad
-// kernel (TLSGPU_SEAL_IMPL=fused), 2 = one lane per chain (=lane).  A/B only.
-static int aes_impl() {  // TLSGPU_SEAL_IMPL, read per launch: split (default) / fused / lane
-    const char* e = getenv("TLSGPU_SEAL_IMPL");
-    return (e && e[0] == 'f') ? 1 : (e && e[0] == 'l') ? 2 : 0;
-}
-static uint32_t debug_skip_flags() {
-    static uint32_t skip = 0xffffffffu;
-    if (skip == 0xffffffffu) {  // TLSGPU_DEBUG_SKIP: 1 = no CBC bulk, 2 = no MAC bulk, bits 4-7 wave priorities, bits 12-13 CBC probes (tg_aes3.h); timing experiments only
-        const char* e = getenv("TLSGPU_DEBUG_SKIP");
-        skip = e ? (uint32_t)atoi(e) : 0u;
-    }
-    return skip;
-}
-// A/B switches for the seal kernels' memory paths, read per launch (tests flip them):
-// TLSGPU_MAC_LOAD=quad -> mac_kernel<.., QL> (quad-cooperative loads), TLSGPU_CBC_IO=16 ->
-// cbc_kernel<NR, IO16> (16-byte I/O).  Defaults (measured faster on cfg2):
-// per-lane MAC loads, column-word CBC I/O.
-static bool env_is(const char* name, char c0) {
-    const char* e = getenv(name);
-    return e && e[0] == c0;
-}
-static int cu_count() {
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (ncu <= 0) ncu = 256;
-    }
-    return ncu;
-}
-
+// ---------------------------------------------------------------- seal launchers
 size_t seal_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * (sizeof(RecMeta) + TAIL_SLOT); }
 
-// phase 1 (stream s1): meta memset + seqnum prefix + per-record MAC / tail / header
+// phase 1 (stream s1): meta memset + seqnum prefix + per-record MAC / tail / header.
+// NR 0 = 3DES (8-byte blocks)
 template <int NR, int MAC, bool SSL3>
 static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
                                    int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s) {
-    // NR 0 = 3DES (8-byte blocks)
     constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
     constexpr int BS = NR == 0 ? 8 : 16;
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
@@ -513,10 +405,8 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((prefix_kernel<CID, MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains,
                        recs, states, wire_len, meta, nrecords, epoch);
-    auto mk = (BS == 16 && env_is("TLSGPU_MAC_LOAD", 'q')) ? mac_kernel<MAC, SSL3, true, BS>
-                                                           : mac_kernel<MAC, SSL3, false, BS>;
-    hipLaunchKernelGGL(mk, dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords, pt, wire, states, wire_len,
-                       meta, tails, epoch, debug_skip_flags());
+    hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS>), dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords, pt,
+                       wire, states, wire_len, meta, tails, epoch);
     return hipGetLastError();
 }
 
@@ -524,97 +414,50 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
 template <int NR>
 static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
-                                   uint8_t* ws, uint32_t epoch, hipStream_t s, int cus = 0) {
-    // cus > 0: the stream is CU-masked to that many CUs (pipeline with TLSGPU_PIPE_MAC_CUS)
-    const uint32_t ncu = cus > 0 ? (uint32_t)cus : (uint32_t)cu_count();
+                                   uint8_t* ws, uint32_t epoch, hipStream_t s) {
+    const uint32_t ncu = cu_count();
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
     if constexpr (NR == 0) {  // 3DES: 8 lanes per chain
         uint32_t pw = (nchains + ncu - 1) / ncu;
         pw = pw < 1 ? 1 : (pw > (uint32_t)D8_CHAINS ? (uint32_t)D8_CHAINS : pw);
-        static bool attrd = false;
-        if (!attrd) {
-            hipError_t e = set_lds(tdes8_kernel, DES_LDS_BYTES);
-            if (e != hipSuccess) return e;
-            attrd = true;
-        }
+        hipError_t e = set_lds(tdes8_kernel, DES_LDS_BYTES);
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL(tdes8_kernel, dim3((nchains + pw - 1) / pw), dim3(D8_THREADS), DES_LDS_BYTES, s, chains,
                            nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch);
         return hipGetLastError();
     } else {
-        // TLSGPU_CBC_ILP (read per launch): 1 = cbc_kernel (16 waves, 1 chain per quad), 2 = cbc2_kernel
-        // (8 waves, 2 chains per quad)
-        const char* ilp_env = getenv("TLSGPU_CBC_ILP");
-        const int ilp = (ilp_env && atoi(ilp_env) == 2) ? 2 : 1;
-        // TLSGPU_CBC_LAYOUT (read per launch): "pair" = cbcp_kernel (2 lanes per chain, up to 512
-        // chains per CU; A/B only: 5 % slower on cfg2, 8 % on cfg3, same box), otherwise the quad
-        // layout cbc_kernel / cbc2_kernel (4 lanes per chain)
-        const char* lay_env = getenv("TLSGPU_CBC_LAYOUT");
-        // on a CU-masked stream (cus > 0) more than 256 chains per CU need the pair layout (one
-        // workgroup generation); on the whole chip extra chains run as further generations
-        const bool quad = (!(lay_env && lay_env[0] == 'p') || ilp == 2 || env_is("TLSGPU_CBC_IO", '1')) &&
-                          (cus <= 0 || (nchains + ncu - 1) / ncu <= (uint32_t)C3_CHAINS);
-        if (!quad) {
-            uint32_t pw = (nchains + ncu - 1) / ncu;
-            pw = pw < 1 ? 1 : (pw > (uint32_t)CP_CHAINS ? (uint32_t)CP_CHAINS : pw);
-            auto kern = cbcp_kernel<NR>;
-            static bool attrp = false;
-            if (!attrp) {
-                hipError_t e = set_lds(kern, AES_LDS_BYTES);
-                if (e != hipSuccess) return e;
-                attrp = true;
-            }
-            hipLaunchKernelGGL(kern, dim3((nchains + pw - 1) / pw), dim3(CP_THREADS), AES_LDS_BYTES, s, chains, nchains,
-                               recs, nrecords, pt, wire, states, meta, tails, pw, epoch, debug_skip_flags());
-            return hipGetLastError();
-        }
         uint32_t cpw = (nchains + ncu - 1) / ncu;
         cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
-        if (ilp == 2) {
-            auto kern = cbc2_kernel<NR>;
-            static bool attr2 = false;
-            if (!attr2) {
-                hipError_t e = set_lds(kern, AES_LDS_BYTES);
-                if (e != hipSuccess) return e;
-                attr2 = true;
-            }
-            hipLaunchKernelGGL(kern, dim3((nchains + cpw - 1) / cpw), dim3(C2_THREADS), AES_LDS_BYTES, s, chains, nchains,
-                               recs, nrecords, pt, wire, states, meta, tails, cpw, epoch, debug_skip_flags());
-            return hipGetLastError();
-        }
-        const bool io16 = env_is("TLSGPU_CBC_IO", '1');
-        auto kern = io16 ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
-        static bool attr[2] = {false, false};
-        if (!attr[io16]) {
-            hipError_t e = set_lds(kern, AES_LDS_BYTES);
-            if (e != hipSuccess) return e;
-            attr[io16] = true;
-        }
+        auto kern = cbc_kernel<NR>;
+        hipError_t e = set_lds(kern, AES_LDS_BYTES);
+        if (e != hipSuccess) return e;
         // persistent: at most one workgroup per CU, quads loop over chain generations
         uint32_t grid = (nchains + cpw - 1) / cpw;
         grid = grid > ncu ? ncu : grid;
         hipLaunchKernelGGL(kern, dim3(grid), dim3(C3_THREADS), AES_LDS_BYTES, s, chains, nchains, recs, nrecords, pt,
-                           wire, states, meta, tails, cpw, epoch, debug_skip_flags());
+                           wire, states, meta, tails, cpw, epoch);
         return hipGetLastError();
     }
 }
 
-template <int NR, int MAC, bool SSL3>
-static hipError_t launch_seal_split(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
-                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
-                                    int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s) {
-    hipError_t e = launch_mac_phase<NR, MAC, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,
-                                                   epoch, s);
-    if (e != hipSuccess) return e;
-    return launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s);
-}
+// The (cipher, MAC, SSL3) variants of the split seal path (AES and 3DES suites)
+#define TG_SPLIT_VARIANTS(X)                             \
+    X(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)   \
+    X(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, false)   \
+    X(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA256, false) \
+    X(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false) \
+    X(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)    \
+    X(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)    \
+    X(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, false)      \
+    X(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, true)
 
-// Split AES seal with the two phases on two streams (pipeline API).
+// Split seal with the two phases on two streams (pipeline API; s1 == s2 for one stream).
 hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
                               const tlsgpu_record* recs, uint32_t nrecords, const uint8_t* pt, uint8_t* wire,
                               ConnState* states, int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s1,
                               hipEvent_t mac_done, hipStream_t s2, hipEvent_t cbc_start, hipEvent_t cbc_stop,
-                              bool* known, int cbc_cus) {
+                              bool* known) {
     *known = true;
     hipError_t e = hipSuccess;
 #define TG_PH(CID, NR, MAC_ID, SSL3)                                                                            \
@@ -622,105 +465,53 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
         e = launch_mac_phase<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,   \
                                                epoch, s1);                                                       \
         if (e != hipSuccess) return e;                                                                           \
-        if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                          \
-        if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                                   \
+        if (s2 != s1) {                                                                                          \
+            if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                      \
+            if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                               \
+        }                                                                                                        \
         if (cbc_start && (e = hipEventRecord(cbc_start, s2)) != hipSuccess) return e;                           \
-        e = launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s2, cbc_cus);     \
+        e = launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s2);              \
         if (e == hipSuccess && cbc_stop) e = hipEventRecord(cbc_stop, s2);                                       \
         return e;                                                                                                \
     }
-    TG_PH(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)
-    TG_PH(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, false)
-    TG_PH(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA256, false)
-    TG_PH(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false)
-    TG_PH(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)
-    TG_PH(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)
-    TG_PH(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, false)
-    TG_PH(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, true)
+    TG_SPLIT_VARIANTS(TG_PH)
 #undef TG_PH
     *known = false;
     return hipSuccess;
 }
 
-template <int NR, int MAC, bool SSL3>
-static hipError_t launch_seal_aesq(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
-                                   const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
-                                   hipStream_t s) {
-    auto kern = seal_aesq_kernel<NR, MAC, SSL3>;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = set_lds(kern, Q_LDS_BYTES);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    const uint32_t ncu = (uint32_t)cu_count();
-    uint32_t cpw = (nchains + ncu - 1) / ncu;
-    cpw = cpw < 1 ? 1 : (cpw > (uint32_t)Q_CHAINS ? (uint32_t)Q_CHAINS : cpw);
-    dim3 grid((nchains + cpw - 1) / cpw);
-    const uint32_t skip = debug_skip_flags();
-    hipLaunchKernelGGL(kern, grid, dim3(Q_THREADS), Q_LDS_BYTES, s, chains, nchains, recs, pt, wire, states, wire_len,
-                       cpw, skip);
-    return hipGetLastError();
-}
-
-template <class C, int MAC, bool SSL3>
-static hipError_t launch_seal_t(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
-                                uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
-                                int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s) {
-    if constexpr (CipherTraits<C>::ID == TLSGPU_CIPHER_AES128 || CipherTraits<C>::ID == TLSGPU_CIPHER_AES256) {
-        constexpr int NR = CipherTraits<C>::ID == TLSGPU_CIPHER_AES128 ? 10 : 14;
-        if (aes_impl() == 0)
-            return launch_seal_split<NR, MAC, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,
-                                                    epoch, s);
-        if (aes_impl() == 1)
-            return launch_seal_aesq<NR, MAC, SSL3>(chains, nchains, recs, pt, wire, states, wire_len, s);
-    }
-    if constexpr (CipherTraits<C>::ID == TLSGPU_CIPHER_3DES) {
-        if (aes_impl() == 0)  // split: prefix / MAC / 8-lane 3DES (TLSGPU_SEAL_IMPL=lane: one lane per chain)
-            return launch_seal_split<0, MAC, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,
-                                                   epoch, s);
-    }
-    auto kern = seal_kernel<C, MAC, SSL3>;
-    constexpr uint32_t lds = CipherTraits<C>::LDS;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = set_lds(kern, lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    dim3 grid((nchains + SEAL_BLOCK - 1) / SEAL_BLOCK);
-    hipLaunchKernelGGL(kern, grid, dim3(SEAL_BLOCK), lds, s, chains, nchains, recs, pt, wire, states, wire_len);
+template <int MAC, bool SSL3>
+static hipError_t launch_rc4_seal(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                                  const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
+                                  hipStream_t s) {
+    auto kern = rc4_seal_kernel<MAC, SSL3>;
+    hipError_t e = set_lds(kern, RC4_LDS_BYTES);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((nchains + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), RC4_LDS_BYTES, s, chains,
+                       nchains, recs, pt, wire, states, wire_len);
     return hipGetLastError();
 }
 
 bool seal_needs_workspace(uint32_t variant) {
     const uint32_t c = variant & 0xff;
-    return aes_impl() == 0 && (c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256 || c == TLSGPU_CIPHER_3DES);
+    return c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256 || c == TLSGPU_CIPHER_3DES;
 }
 
 hipError_t launch_seal(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                        uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
                        uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known) {
+    if (seal_needs_workspace(variant))
+        return launch_seal_phases(variant, chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws, epoch, s,
+                                  nullptr, s, nullptr, nullptr, known);
     *known = true;
-#define TG_SEAL_CASE(CIPHER_ID, CTYPE, MAC_ID, SSL3)                                                      \
-    if (variant == TLSGPU_VARIANT(CIPHER_ID, MAC_ID, SSL3))                                               \
-        return launch_seal_t<CTYPE, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws, \
-                                                  epoch, s);
-    // TLS 1.0-1.2 HMAC suites (constants.py:159-201)
-    TG_SEAL_CASE(TLSGPU_CIPHER_AES128, AesCbc<10>, TLSGPU_MAC_SHA1, false)
-    TG_SEAL_CASE(TLSGPU_CIPHER_AES256, AesCbc<14>, TLSGPU_MAC_SHA1, false)
-    TG_SEAL_CASE(TLSGPU_CIPHER_AES128, AesCbc<10>, TLSGPU_MAC_SHA256, false)
-    TG_SEAL_CASE(TLSGPU_CIPHER_AES256, AesCbc<14>, TLSGPU_MAC_SHA256, false)
-    TG_SEAL_CASE(TLSGPU_CIPHER_3DES, TdesCbc, TLSGPU_MAC_SHA1, false)
-    TG_SEAL_CASE(TLSGPU_CIPHER_RC4, Rc4Stream, TLSGPU_MAC_SHA1, false)
-    TG_SEAL_CASE(TLSGPU_CIPHER_RC4, Rc4Stream, TLSGPU_MAC_MD5, false)
-    // SSL 3.0 MAC_SSL suites (mathtls.py:125-151)
-    TG_SEAL_CASE(TLSGPU_CIPHER_AES128, AesCbc<10>, TLSGPU_MAC_SHA1, true)
-    TG_SEAL_CASE(TLSGPU_CIPHER_AES256, AesCbc<14>, TLSGPU_MAC_SHA1, true)
-    TG_SEAL_CASE(TLSGPU_CIPHER_3DES, TdesCbc, TLSGPU_MAC_SHA1, true)
-    TG_SEAL_CASE(TLSGPU_CIPHER_RC4, Rc4Stream, TLSGPU_MAC_SHA1, true)
-    TG_SEAL_CASE(TLSGPU_CIPHER_RC4, Rc4Stream, TLSGPU_MAC_MD5, true)
-#undef TG_SEAL_CASE
+#define TG_RC4_CASE(MAC_ID, SSL3)                       \
+    if (variant == TLSGPU_VARIANT(TLSGPU_CIPHER_RC4, MAC_ID, SSL3)) \
+        return launch_rc4_seal<MAC_ID, SSL3>(chains, nchains, recs, pt, wire, states, wire_len, s);
+    TG_RC4_CASE(TLSGPU_MAC_SHA1, false)
+    TG_RC4_CASE(TLSGPU_MAC_MD5, false)
+    TG_RC4_CASE(TLSGPU_MAC_SHA1, true)
+    TG_RC4_CASE(TLSGPU_MAC_MD5, true)
+#undef TG_RC4_CASE
     *known = false;
     return hipSuccess;
 }
@@ -732,16 +523,11 @@ static hipError_t launch_cipher_t(const tlsgpu_span* spans, uint32_t n, const ui
     constexpr bool AES = CIPHER == TLSGPU_CIPHER_AES128 || CIPHER == TLSGPU_CIPHER_AES256 ||
                          CIPHER == TLSGPU_CIPHER_AES192;
     constexpr uint32_t lds = AES ? (DEC ? AES_DEC_LDS_BYTES : AES_LDS_BYTES)
-                                 : CIPHER == TLSGPU_CIPHER_3DES ? DES_LDS_BYTES
-                                                                : RC4_LDS_BYTES_PER_WAVE * (SEAL_BLOCK / 64);
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = set_lds(kern, lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    dim3 grid((n + SEAL_BLOCK - 1) / SEAL_BLOCK);
-    hipLaunchKernelGGL(kern, grid, dim3(SEAL_BLOCK), lds, s, spans, n, in, out, states);
+                                 : CIPHER == TLSGPU_CIPHER_3DES ? DES_LDS_BYTES : RC4_LDS_BYTES;
+    hipError_t e = set_lds(kern, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((n + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), lds, s, spans, n, in, out,
+                       states);
     return hipGetLastError();
 }
 
@@ -778,15 +564,13 @@ hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, 
     return hipGetLastError();
 }
 
-
-// ---------------------------------------------------------------- block-parallel AES open
+// ---------------------------------------------------------------- open launchers
 size_t open_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * sizeof(OpenMeta); }
 
+// AES suites (every AES variant: SHA1 TLS/SSL3, SHA256 TLS 1.2) open block-parallel
 static bool open_split_variant(uint32_t v) {
-    const uint32_t c = v & 0xff, m = (v >> 8) & 0xff, ssl3 = (v >> 16) & 1;
-    const bool aes = c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256;
-    return aes && (m == TLSGPU_MAC_SHA1 || (m == TLSGPU_MAC_SHA256 && !ssl3)) && !(getenv("TLSGPU_OPEN_IMPL") &&
-                                                                                   !strcmp(getenv("TLSGPU_OPEN_IMPL"), "lane"));
+    const uint32_t c = v & 0xff;
+    return c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256;
 }
 bool open_needs_workspace(uint32_t variant) { return open_split_variant(variant); }
 
@@ -802,40 +586,47 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
     hipLaunchKernelGGL((open_prefix_kernel<CID, MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords,
                        wire, states, status, meta, epoch);
     auto dec = open_dec_kernel<NR>;
-    static bool attr = false;
-    if (!attr) {
-        if ((e = set_lds(dec, AES_DEC_LDS_BYTES)) != hipSuccess) return e;
-        attr = true;
-    }
+    if ((e = set_lds(dec, AES_DEC_LDS_BYTES)) != hipSuccess) return e;
     uint32_t grid = (nrecords + (O3_THREADS / 64) - 1) / (O3_THREADS / 64);
-    grid = grid > (uint32_t)cu_count() ? (uint32_t)cu_count() : (grid ? grid : 1u);
+    grid = grid > cu_count() ? cu_count() : (grid ? grid : 1u);
     hipLaunchKernelGGL(dec, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s, recs, nrecords, wire, pt, states, meta,
                        epoch);
     hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords, pt, states,
                        status, meta, epoch);
     hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status, meta,
                        epoch);
+    hipLaunchKernelGGL(open_stop_kernel, gc, dim3(256), 0, s, chains, nchains, recs, nrecords, wire, states, status,
+                       meta, epoch);
     return hipGetLastError();
 }
 
 hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
                        const tlsgpu_open_record* recs, uint32_t nrecords, const uint8_t* wire, uint8_t* pt,
                        ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known) {
-    if (open_split_variant(variant)) {
-        *known = true;
+    *known = true;
 #define TG_OPEN3(CID, NR, MAC_ID, SSL3)                                                                         \
-        if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3))                                                       \
-            return launch_open_split<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, wire, pt, states, status, \
-                                                        ws, epoch, s);
-        TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)
-        TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, false)
-        TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA256, false)
-        TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false)
-        TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)
-        TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)
+    if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3))                                                           \
+        return launch_open_split<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, wire, pt, states, status, ws, \
+                                                    epoch, s);
+    TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)
+    TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, false)
+    TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA256, false)
+    TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false)
+    TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)
+    TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)
 #undef TG_OPEN3
-    }
-    return launch_open_lane(variant, chains, nchains, recs, wire, pt, states, status, s, known);
+#define TG_OPEN_CASE(CIPHER_ID, MAC_ID, SSL3)                 \
+    if (variant == TLSGPU_VARIANT(CIPHER_ID, MAC_ID, SSL3)) \
+        return launch_open_t<CIPHER_ID, MAC_ID, SSL3>(chains, nchains, recs, wire, pt, states, status, s);
+    TG_OPEN_CASE(TLSGPU_CIPHER_3DES, TLSGPU_MAC_SHA1, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_SHA1, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_MD5, false)
+    TG_OPEN_CASE(TLSGPU_CIPHER_3DES, TLSGPU_MAC_SHA1, true)
+    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_SHA1, true)
+    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_MD5, true)
+#undef TG_OPEN_CASE
+    *known = false;
+    return hipSuccess;
 }
 
 }  // namespace tg

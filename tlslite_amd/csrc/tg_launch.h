@@ -16,7 +16,7 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
                               const tlsgpu_record* recs, uint32_t nrecords, const uint8_t* pt, uint8_t* wire,
                               ConnState* states, int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s1,
                               hipEvent_t mac_done, hipStream_t s2, hipEvent_t cbc_start, hipEvent_t cbc_stop,
-                              bool* known, int cbc_cus = 0);
+                              bool* known);
 hipError_t launch_cipher(int cipher, int dec, const tlsgpu_span* spans, uint32_t n, const uint8_t* in, uint8_t* out,
                          ConnState* states, hipStream_t s, bool* known);
 size_t open_workspace_bytes(uint32_t nrecords);

@@ -18,6 +18,11 @@
 //                       computed and so whether a seqnum is consumed (:1018).
 //   open_mac_kernel     one lane per record: MAC over the plaintext, compare
 //                       (:1006-1039), status.
+//   open_stop_kernel    one lane per chain, TLSGPU_CHAIN_STOP_ON_ALERT chains
+//                       only: records after the first alert become
+//                       TLSGPU_ALERT_SKIPPED and the state is rolled back to
+//                       what the failing record left (the reference closes the
+//                       connection at the alert, :1039-1042).
 //
 // Workspace per record: one 48-byte OpenMeta.
 #pragma once
@@ -27,7 +32,7 @@ namespace tg {
 
 struct OpenMeta {
     uint32_t pred[4];  // ciphertext block before this record's first block (CBC residue)
-    uint64_t seq;
+    uint64_t seq;      // seqnum before this record (the MAC's seqnum when OM_VERIFY)
     uint32_t state;
     uint32_t epoch;
     uint32_t flags;  // OM_*
@@ -168,7 +173,7 @@ open_dec_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
         const uint32_t nb = R.ct_len >> 4;
         const uint8_t* C = wire + R.ct_off + 4 * q;
         uint8_t* P = pt + R.pt_off + 4 * q;
-        const bool al = ((R.ct_off | R.pt_off) & 3) == 0;
+        const bool al = (((uintptr_t)(wire + R.ct_off) | (uintptr_t)(pt + R.pt_off)) & 3) == 0;
         const uint32_t pq = mt.pred[q];
         for (uint32_t b0 = 0; b0 < nb; b0 += 32) {
             const uint32_t ba = b0 + quad, bb = b0 + 16 + quad;
@@ -201,8 +206,10 @@ __global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __res
         const uint32_t r = ch.first + k;
         if (r >= nrecords) break;
         OpenMeta& m = meta[r];
-        if (m.epoch != epoch || !(m.flags & OM_DEC)) continue;
+        if (m.epoch != epoch) continue;
         any = true;
+        m.seq = seq;
+        if (!(m.flags & OM_DEC)) continue;
         const uint8_t* P = pt + recs[r].pt_off;
         const uint32_t len = m.len;
         const uint32_t pl = P[len - 1];
@@ -224,7 +231,7 @@ __global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __res
             m.flags = 0;
         } else {
             m.n = len - endLen;
-            m.seq = seq++;  // getSeqNumBytes (:1018)
+            seq++;  // getSeqNumBytes (:1018)
             m.flags = OM_DEC | OM_VERIFY | (padGood ? OM_PADOK : 0u);
         }
     }
@@ -261,6 +268,36 @@ __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record*
     for (int i = 0; i < DL; i++)
         if (P[n + i] != (uint8_t)(m[i >> 2] >> (8 * (i & 3)))) macGood = false;
     status[r] = ((mt.flags & OM_PADOK) && macGood) ? (int32_t)n : TLSGPU_ALERT_BAD_RECORD_MAC;
+}
+
+__global__ void __launch_bounds__(256) open_stop_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
+                                                       const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
+                                                       const uint8_t* __restrict__ wire, ConnState* __restrict__ states,
+                                                       int32_t* __restrict__ status,
+                                                       const OpenMeta* __restrict__ meta, uint32_t epoch) {
+    const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cid >= nchains) return;
+    const tlsgpu_chain ch = chains[cid];
+    if (!(ch.flags & TLSGPU_CHAIN_STOP_ON_ALERT)) return;
+    for (uint32_t k = 0; k < ch.count; k++) {
+        const uint32_t r = ch.first + k;
+        if (r >= nrecords) return;
+        const int32_t s = status[r];
+        if (s != TLSGPU_ALERT_BAD_RECORD_MAC && s != TLSGPU_ALERT_DECRYPTION_FAILED) continue;
+        const OpenMeta& m = meta[r];
+        if (m.epoch != epoch || k + 1 == ch.count) return;
+        for (uint32_t j = k + 1; j < ch.count && ch.first + j < nrecords; j++) status[ch.first + j] = TLSGPU_ALERT_SKIPPED;
+        // state as record r left it: its seqnum was consumed iff its MAC was computed, and its
+        // last ciphertext block is the residue iff it was decrypted (a block multiple)
+        ConnState* st = states + m.state;
+        st->seqnum = m.seq + ((m.flags & OM_VERIFY) ? 1u : 0u);
+        const tlsgpu_open_record R = recs[r];
+        uint32_t res[4] = {m.pred[0], m.pred[1], m.pred[2], m.pred[3]};
+        if (R.ct_len && !(R.ct_len & 15u)) load16(wire + R.ct_off + R.ct_len - 16, res);
+#pragma unroll
+        for (int i = 0; i < 4; i++) st->iv[i] = res[i];
+        return;
+    }
 }
 
 }  // namespace tg

@@ -1,0 +1,107 @@
+// tg_quad.h -- the AES round laid out for a CDNA4 quad of lanes.
+//
+// 4 lanes per AES block ("quad"): lane q holds state column q.  A round is 4
+// conflict-free LDS T-table lookups per lane (one v_perm_b32 builds each
+// address from the state word and a per-lane bank-copy offset) combined by an
+// XOR tree across the quad whose lane exchanges ride in the DPP operand of
+// v_xor_b32 (rijndael.py:304-310 restated for the quad).
+//
+// LDS: [0, 128K) the 4 T-tables x 32 lane copies in the layout of aes_lds_fill
+// (T0/T1 rows in the low 64K, T2/T3 in the high 64K).
+#pragma once
+#include "tg_device.h"
+
+namespace tg {
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+
+__device__ __forceinline__ uint32_t lds_read32(uint32_t addr) { return *(const lds_u32_t*)(size_t)addr; }
+
+// v_xor_b32_dpp-able quad permutation (update_dpp with old=0 lets the DPP
+// combiner fold the move into the consuming XOR)
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+
+struct QuadAes {
+    uint32_t lo, hi;  // lane-copy offset words (table pair select in byte 2)
+    __device__ __forceinline__ void init() {
+        lo = (__lane_id() & 31) * 4;
+        hi = lo | 0x10000u;
+    }
+    template <int T, int B>  // T_t[byte B of s]
+    __device__ __forceinline__ uint32_t look(uint32_t s) const {
+        constexpr uint32_t sel = 0x0c000000u | (2u << 16) | ((4u + B) << 8) | 0u;
+        return lds_read32(perm(s, T >= 2 ? hi : lo, sel) + (T & 1) * 128);
+    }
+    // Column q of the next state = T0[b0(q)] ^ T1[b1(q+1)] ^ T2[b2(q+2)] ^ T3[b3(q+3)] ^ k[q], with
+    // the lookup of byte b done by lane q+b.  XOR tree: dpp2(t2) ^ dpp3(t3) = dpp2(t2 ^ dpp1(t3)),
+    // and the round key rides in that inner term: k2 is the key column of lane q+2 (round_keys()),
+    // so once the T0/T1 lookups return only two dependent DPP XORs remain (a chain needs four).
+    // The T2/T3 lookups are issued first: they feed the inner term.
+    __device__ __forceinline__ uint32_t round(uint32_t x, uint32_t k2) const {
+        const uint32_t t2 = look<2, 2>(x);
+        const uint32_t t3 = look<3, 3>(x);
+        const uint32_t t0 = look<0, 0>(x);
+        const uint32_t t1 = look<1, 1>(x);
+#ifdef TG_AB_ROUND_B
+        // one DPP XOR after the last lookup: ((k ^ dpp2 t2) ^ dpp3 t3) ^ t0 ^ dpp1 t1, with
+        // k2 = the key column of lane q+2 moved back by the first DPP (tools/build_ab.sh)
+        const uint32_t a = quad_dpp<0x4E>(t2 ^ k2);
+        const uint32_t w = a ^ quad_dpp<0x93>(t3);
+        return (t0 ^ w) ^ quad_dpp<0x39>(t1);
+#else
+        const uint32_t u = (t2 ^ k2) ^ quad_dpp<0x39>(t3);
+        const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
+        return z ^ quad_dpp<0x4E>(u);
+#endif
+    }
+    // per-lane round keys in the layout round()/last() expect: k[0] = whitening column q,
+    // k[r >= 1] = column (q+2)&3 of round key r
+    template <int NR>
+    static __device__ __forceinline__ void round_keys(const uint32_t* ek, uint32_t q, uint32_t* k) {
+        k[0] = ek[q];
+#pragma unroll
+        for (int r = 1; r <= NR; r++) k[r] = ek[4 * r + ((q + 2) & 3)];
+    }
+    __device__ __forceinline__ uint32_t last(uint32_t x, uint32_t k) const {
+        // S-box byte r sits at byte r of table (r+2)&3
+        const uint32_t s2 = look<0, 2>(x) & 0xff0000u;
+        const uint32_t s3 = look<1, 3>(x) & 0xff000000u;
+        const uint32_t s0 = look<2, 0>(x) & 0xffu;
+        const uint32_t s1 = look<3, 1>(x) & 0xff00u;
+        const uint32_t u = (s2 ^ k) ^ quad_dpp<0x39>(s3);
+        const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
+        return z ^ quad_dpp<0x4E>(u);
+    }
+    // one block of one chain
+    template <int NR>
+    __device__ __forceinline__ uint32_t encrypt1(uint32_t a, const uint32_t* ka) const {
+        a ^= ka[0];
+#pragma unroll
+        for (int r = 1; r < NR; r++) a = round(a, ka[r]);
+        return last(a, ka[NR]);
+    }
+    // one block whose input is already whitened (x = block ^ k[0])
+    template <int NR>
+    __device__ __forceinline__ uint32_t encrypt_w(uint32_t a, const uint32_t* ka) const {
+#pragma unroll
+        for (int r = 1; r < NR; r++) a = round(a, ka[r]);
+        return last(a, ka[NR]);
+    }
+};
+
+__device__ __forceinline__ uint32_t ld32(const uint8_t* p, bool al) {
+    if (al) return *(const uint32_t*)p;
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ void st32(uint8_t* p, uint32_t v, bool al) {
+    if (al) {
+        *(uint32_t*)p = v;
+    } else {
+        p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+    }
+}
+
+}  // namespace tg

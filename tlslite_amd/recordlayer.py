@@ -99,14 +99,14 @@ def make_records(pt_off, wire_off, pt_len, content_type=ContentType.application_
     return recs
 
 
-def make_chains(state_idx, first, count):
+def make_chains(state_idx, first, count, flags=0):
     n = len(state_idx)
     ch = (N.Chain * n)()
     a = np.frombuffer(ch, dtype=np.uint32).reshape(n, 4)
     a[:, 0] = state_idx
     a[:, 1] = first
     a[:, 2] = count
-    a[:, 3] = 0
+    a[:, 3] = flags
     return ch
 
 
@@ -281,15 +281,21 @@ def open_dev(chains, nchains, records, nrecords, wire, pt, states, status, varia
            stream.handle if stream is not None else None)
 
 
-def open_records(states, records, stream=None):
+def open_records(states, records, stream=None, stop_on_alert=True):
     """Open (decrypt + verify) records on the GPU -- the batched counterpart of
     _decryptRecord (tlsrecordlayer.py:958-1044).
 
     states:  list of read-direction ConnectionState (updated in place)
     records: list of (state_index, content_type, body); records of one state
              are opened in list order.
+    stop_on_alert: a connection stops at its first alert, as the reference's
+             does (_getMsg raises, _sendError closes it, :1039-1042): later
+             records of that state come back as N.ALERT_SKIPPED and the state is
+             left as the failing record left it.  False opens every record, as
+             successive bare _decryptRecord calls would.
     Returns a list of (status, plaintext): status 0 and the plaintext bytes,
-    or an alert code (N.ALERT_BAD_RECORD_MAC / N.ALERT_DECRYPTION_FAILED) and None.
+    or an alert code (N.ALERT_BAD_RECORD_MAC / N.ALERT_DECRYPTION_FAILED /
+    N.ALERT_SKIPPED) and None.
     """
     nrec = len(records)
     if nrec == 0:
@@ -327,7 +333,8 @@ def open_records(states, records, stream=None):
     d_pt.zero(stream)
     keep = []
     for var, chs in buckets.items():
-        c = make_chains([x[0] for x in chs], [x[1] for x in chs], [x[2] for x in chs])
+        c = make_chains([x[0] for x in chs], [x[1] for x in chs], [x[2] for x in chs],
+                        N.CHAIN_STOP_ON_ALERT if stop_on_alert else 0)
         d_ch = DeviceBuffer(ctypes.sizeof(c))
         d_ch.upload(np.frombuffer(c, dtype=np.uint8), stream=stream)
         keep.append(d_ch)

@@ -261,12 +261,12 @@ class Workload:
         var = self.launches[0][0]
         c, m = var & 0xff, (var >> 8) & 0xff
         if c in (N.CIPHER_AES128, N.CIPHER_AES256) and m in (N.MAC_SHA1, N.MAC_SHA256):
-            return "cbc_kernel<%d, false>" % (10 if c == N.CIPHER_AES128 else 14)
+            return "cbc_kernel<%d>" % (10 if c == N.CIPHER_AES128 else 14)
         if c == N.CIPHER_3DES:
             # split path: bench.py's events bracket the whole 3DES seal call (prefix + MAC +
             # tdes8_kernel), which tdes8_kernel dominates
             return "tdes8_kernel"
-        return "seal_kernel"
+        return "rc4_seal_kernel"
 
     def aes_lookups(self):
         """LDS T-table lookups of one seal call when every launch is an AES suite:

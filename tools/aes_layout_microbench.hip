@@ -1,7 +1,7 @@
 // aes_layout_microbench.hip -- AES chains at a fixed number of chains per CU
 // (cfg2: 65,536 independent CBC chains on 256 CUs = 256 per CU), comparing lane
 // layouts of the LDS T-table round with no global-memory traffic in the loop:
-//   quad1   4 lanes/chain, column per lane, XOR tree dpp2(t2^dpp1(t3)) (tg_aesq.h), 16 waves/CU
+//   quad1   4 lanes/chain, column per lane, XOR tree dpp2(t2^dpp1(t3)) (tg_quad.h), 16 waves/CU
 //   quad1b  4 lanes/chain, XOR tree ordered for the last lookup: ((k ^ dpp2 t2) ^ dpp3 t3) ^ t0 ^ dpp1 t1
 //   quad2   4 lanes/chain, 2 chains per quad interleaved,                    8 waves/CU
 //   quad2b  as quad2 with the quad1b XOR order
@@ -9,6 +9,9 @@
 //   pair2   2 lanes/chain, 2 chains per lane pair,                           4 waves/CU
 //   lane1   1 lane/chain (16 lookups per lane),                              4 waves/CU
 //   *@512   the same at 512 chains per CU (cfg3 has 4,096 per CU)
+//   latency mode (argv[2] = "lat"): 2 and 16 chains per CU (cfg4 at 8 GPUs / 1 GPU):
+//   the round is then one chain's dependent latency, reported in shader cycles;
+//   quad1s = quad1b with ONE chain per wave (chains spread over the SIMDs)
 // Every layout encrypts the same chains with the same round keys; the host checks
 // that all final states agree.  Reports ns and shader cycles (s_memtime) per round,
 // the LDS-array floor fraction (16 lookups x chains / 32 per cycle) and the
@@ -18,7 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
-#include "../tlslite_amd/csrc/tg_aesq.h"
+#include "../tlslite_amd/csrc/tg_quad.h"
 #include "../tlslite_amd/csrc/tg_hash.h"
 
 using namespace tg;
@@ -103,7 +106,8 @@ __device__ __forceinline__ uint32_t init_word(uint32_t chain, uint32_t col) {
     return (chain * 2654435761u) ^ (col * 0x9e3779b9u) ^ 0x5bd1e995u;
 }
 
-// LAYOUT: 4 = quad, 5 = quad with round_b, 2 = pair, 1 = lane.  CPC = chains per CU.
+// LAYOUT: 4 = quad, 5 = quad with round_b, 6 = round_b with one chain per wave, 2 = pair,
+// 1 = lane.  CPC = chains per CU.
 // out[chain*4 + col] = final state; cyc[block] = s_memtime delta of wave 0
 template <int LAYOUT, int ILP, int CPC>
 __global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict__ ek, uint32_t* __restrict__ out,
@@ -113,11 +117,12 @@ __global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict_
     __builtin_amdgcn_s_setprio(1);  // as cbc_kernel: win issue arbitration over the MAC waves
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if constexpr (LAYOUT == 4 || LAYOUT == 5) {  // quad: lane q = column q
+    if constexpr (LAYOUT == 4 || LAYOUT == 5 || LAYOUT == 6) {  // quad: lane q = column q
         QuadAesB L;
         L.init();
         const uint32_t q = lane & 3;
-        const uint32_t quad = wave * 16 + (lane >> 2);
+        const uint32_t quad = LAYOUT == 6 ? wave : wave * 16 + (lane >> 2);
+        if (LAYOUT == 6 && lane >= 4) return;
         uint32_t k[NR + 1];
         if constexpr (LAYOUT == 4) {
             QuadAes::round_keys<NR>(ek, q, k);
@@ -139,7 +144,7 @@ __global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict_
             for (int r = 1; r < NR; r++) {
                 uint32_t y[ILP];
 #pragma unroll
-                for (int i = 0; i < ILP; i++) y[i] = LAYOUT == 4 ? L.round<0>(x[i], k[r]) : L.round_b(x[i], k[r]);
+                for (int i = 0; i < ILP; i++) y[i] = LAYOUT == 4 ? L.round(x[i], k[r]) : L.round_b(x[i], k[r]);
 #pragma unroll
                 for (int i = 0; i < ILP; i++) x[i] = y[i];
             }
@@ -245,7 +250,7 @@ static uint32_t* g_side_out = nullptr;
 
 template <int LAYOUT, int ILP, int CPC>
 static Res run(const char* name, const uint32_t* d_ek, int cus, int blocks, int corun = 0) {
-    const int lanes_per_chain = LAYOUT >= 4 ? 4 : LAYOUT;
+    const int lanes_per_chain = LAYOUT == 6 ? 64 : LAYOUT >= 4 ? 4 : LAYOUT;
     const int threads = CPC * lanes_per_chain / ILP;
     auto kern = bench_kernel<LAYOUT, ILP, CPC>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -285,9 +290,10 @@ static Res run(const char* name, const uint32_t* d_ek, int cus, int blocks, int 
     const double rounds = (double)blocks * NR;
     const double floor_cyc = CPC * 16.0 / 32.0;  // LDS-array cycles per round
     const double ns = r.ms * 1e6 / rounds;
-    printf("%-7s chains/CU=%3d waves/CU=%2d%s  %7.2f ns/round  clock %.2f GHz  %5.1f G lookups/s/CU  "
+    // loop cycles (s_memtime of wave 0 around the block loop, table fill excluded)
+    printf("%-7s chains/CU=%3d waves/CU=%2d%s  %7.2f ns/round  %6.1f loop-cyc/round  clock %.2f GHz  %5.1f G lookups/s/CU  "
            "LDS-floor frac %.2f  cfg2-equiv %.3f ms\n",
-           name, CPC, threads / 64, corun ? " +sha" : "     ", ns, ghz, CPC * 16.0 / ns,
+           name, CPC, (threads + 63) / 64, corun ? " +sha" : "     ", ns, r.cyc / rounds, ghz, CPC * 16.0 / ns,
            floor_cyc / (ns * ghz), r.ms * (256.0 / CPC) * 1027.0 / blocks);
     fflush(stdout);
     return r;
@@ -316,6 +322,22 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(d_ek, ek, sizeof(ek), hipMemcpyHostToDevice);
     (void)hipStreamCreateWithFlags(&g_side, hipStreamNonBlocking);
     (void)hipMalloc(&g_side_out, (size_t)cus * 256 * 4);
+    if (argc > 2 && argv[2][0] == 'l') {  // latency regime (cfg4)
+        std::vector<Res> l2, l16;
+        l2.push_back(run<4, 1, 2>("quad1", d_ek, cus, blocks));
+        l2.push_back(run<5, 1, 2>("quad1b", d_ek, cus, blocks));
+        l2.push_back(run<6, 1, 2>("quad1s", d_ek, cus, blocks));
+        l2.push_back(run<2, 1, 2>("pair1", d_ek, cus, blocks));
+        l2.push_back(run<1, 1, 2>("lane1", d_ek, cus, blocks));
+        l16.push_back(run<4, 1, 16>("quad1", d_ek, cus, blocks));
+        l16.push_back(run<5, 1, 16>("quad1b", d_ek, cus, blocks));
+        l16.push_back(run<6, 1, 16>("quad1s", d_ek, cus, blocks));
+        l16.push_back(run<2, 1, 16>("pair1", d_ek, cus, blocks));
+        l16.push_back(run<1, 1, 16>("lane1", d_ek, cus, blocks));
+        const int bad = compare(l2) | compare(l16);
+        if (!bad) printf("all layouts agree\n");
+        return bad;
+    }
     std::vector<Res> a;
     a.push_back(run<4, 1, 256>("quad1", d_ek, cus, blocks));
     a.push_back(run<5, 1, 256>("quad1b", d_ek, cus, blocks));
