@@ -145,58 +145,58 @@ def oracle_check(wl, wire_gpu, nthreads, sample=None, min_seconds=0.0):
     return ok, dt, len(recs), int(wl.pt_len[recs].sum()) * reps, nthreads, reps
 
 
-def host_inclusive_rate(wl, nsub=16):
-    """Plaintext GiB/s including pinned H2D of plaintext + seal + D2H of wire,
-    pipelined over `nsub` sub-batches on 3 streams (copies overlap kernels)."""
-    import ctypes
+PCIE_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s per direction (spec)
+
+
+def host_inclusive_rate(wl, chunk=32 << 20, depth=3):
+    """Plaintext GiB/s with the records starting and ending in HOST memory, through the
+    C host pipeline (tlsgpu_host_pipeline_seal: H2D of plaintext, seal, D2H of the
+    wire arena, sub-batches overlapped on `depth` streams), for pinned host arenas and
+    for pageable ones (staged through the library's pinned buffers).  The wire output
+    of both is compared with the device-resident path's.  Never `value`."""
     from tlslite_amd import _native as N
-    from tlslite_amd.device import Event, PinnedBuffer, Stream, synchronize
+    from tlslite_amd.constants import ContentType
+    from tlslite_amd.device import PinnedBuffer, synchronize
+    from tlslite_amd.recordlayer import HostSealPipeline, make_chains, make_records
     if len(wl.launches) != 1:
         return None
-    var, _, nch = wl.launches[0]
-    if nch != wl.n_records:  # only for one-record chains laid out in order
-        return None
-    from tlslite_amd.recordlayer import make_chains
-    from tlslite_amd.device import DeviceBuffer
-    pin_pt = PinnedBuffer(wl.pt_bytes)
-    pin_wire = PinnedBuffer(wl.wire_bytes)
+    var = wl.launches[0][0]
+    recs = make_records(wl.pt_off, wl.wire_off, wl.pt_len, ContentType.application_data, 0)
+    chains = make_chains(np.arange(wl.n_chains, dtype=np.uint32), wl.chain_first, wl.chain_count)
+    # reference output: the device-resident path from the initial states
+    wl.reset_states()
+    wl.launch()
+    synchronize()
+    ref = wl.d_wire.download()
+    pin_pt, pin_wire = PinnedBuffer(wl.pt_bytes), PinnedBuffer(wl.wire_bytes)
     wl.d_pt.download(out=pin_pt.array[: wl.pt_bytes])
-    streams = [Stream() for _ in range(3)]
-    per = (wl.n_records + nsub - 1) // nsub
-    subs = []
-    for s in range(nsub):
-        a, b = s * per, min(wl.n_records, (s + 1) * per)
-        if a >= b:
-            break
-        # sub-batch = records [a, b): chains index relative to the sub-range
-        ch = make_chains(np.arange(a, b, dtype=np.uint32), np.arange(0, b - a, dtype=np.uint32),
-                         np.ones(b - a, dtype=np.uint32))
-        d = DeviceBuffer(ctypes.sizeof(ch))
-        d.upload(np.frombuffer(ch, dtype=np.uint8))
-        p0, p1 = int(wl.pt_off[a]), int(wl.pt_off[b - 1]) + int(wl.pt_len[b - 1])
-        w0, w1 = int(wl.wire_off[a]), int(wl.wire_off[b - 1]) + int(wl.wire_len[b - 1])
-        subs.append((d, b - a, p0, p1, w0, w1, a))
-    wss = [DeviceBuffer(int(N.lib.tlsgpu_seal_workspace_bytes(per))) for _ in range(3)]
-    best = None
-    for _rep in range(3):
-        wl.reset_states()
-        synchronize()
-        t0 = time.perf_counter()
-        for i, (d, n, p0, p1, w0, w1, a) in enumerate(subs):
-            st = streams[i % 3]
-            ws = wss[i % 3]
-            N.call("tlsgpu_memcpy_h2d", wl.d_pt.at(p0), ctypes.c_void_p(pin_pt.ptr.value + p0), p1 - p0, st.handle)
-            N.call("tlsgpu_seal_dev", d.ptr, n, wl.d_recs.at(24 * a), n, wl.d_pt.ptr, wl.d_wire.ptr,
-                   wl.d_states.ptr, wl.d_len.at(4 * a), var, ws.ptr, ws.nbytes, st.handle)
-            N.call("tlsgpu_memcpy_d2h", ctypes.c_void_p(pin_wire.ptr.value + w0 - 11), wl.d_wire.at(w0 - 11),
-                   w1 - w0 + 11, st.handle)
-        for st in streams:
-            st.synchronize()
-        dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
-    rate = wl.plaintext_total / GIB / best
-    return {"value": round(rate, 2), "unit": "GiB/s", "ms": round(best * 1e3, 3),
-            "method": "pinned hipMemcpyAsync H2D(plaintext) + seal + D2H(wire), %d sub-batches on 3 streams" % len(subs)}
+    pag_pt, pag_wire = pin_pt.array[: wl.pt_bytes].copy(), np.zeros(wl.wire_bytes, dtype=np.uint8)
+    lens = np.zeros(wl.n_records, dtype=np.int32)
+    out = {"unit": "GiB/s", "chunk_bytes": chunk, "depth": depth,
+           "bytes_h2d": int(wl.pt_bytes), "bytes_d2h": int(wl.wire_bytes),
+           "pcie_ceiling": round(wl.plaintext_total / GIB / (max(wl.pt_bytes, wl.wire_bytes) / (PCIE_GBS * 1e9)), 2),
+           "method": "tlsgpu_host_pipeline_seal: per sub-batch of ~chunk_bytes plaintext H2D copy, seal, D2H copy "
+                     "of its wire range, sub-batches on `depth` streams; wall time of the synchronous call, best of 3; "
+                     "pcie_ceiling = plaintext / (max(H2D, D2H bytes) at 63 GB/s per direction, full duplex)"}
+    with HostSealPipeline(chunk, depth) as hp:
+        for name, pt_h, wire_h in (("pinned", pin_pt.array[: wl.pt_bytes], pin_wire.array[: wl.wire_bytes]),
+                                   ("pageable", pag_pt, pag_wire)):
+            best = None
+            for _rep in range(3):
+                wl.reset_states()
+                synchronize()
+                t0 = time.perf_counter()
+                hp.seal(chains, recs, pt_h, wire_h, wl.d_states, lens, var)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            exact = bool(np.array_equal(wire_h, ref)) and bool(np.array_equal(lens, wl.wire_len.astype(np.int32)))
+            out[name] = {"value": round(wl.plaintext_total / GIB / best, 2), "ms": round(best * 1e3, 3),
+                         "bit_exact": exact}
+    out["value"] = out["pinned"]["value"]
+    out["pcie_frac"] = round(out["value"] / out["pcie_ceiling"], 3)
+    pin_pt.free()
+    pin_wire.free()
+    return out
 
 
 def open_rate(wl, stream, steps):

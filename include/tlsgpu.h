@@ -14,6 +14,9 @@
  *                              MAC :567-586, explicit IV :594-595, padding
  *                              :597-606, encrypt :608/:613, header :616-617),
  *                              batched over many records / connections
+ *   tlsgpu_host_pipeline_seal  the same from host socket buffers: the whole
+ *                              write path of :538-620 (seal + the socket-buffer
+ *                              hand-off) with the PCIe copies overlapped
  *   tlsgpu_open_dev .......... tlsrecordlayer.py:958-1044 (_decryptRecord)
  *   tlsgpu_cipher_dev ........ utils/python_aes.py:20-69, utils/python_rc4.py:25-41,
  *                              utils/openssl_tripledes.py:29-47 (the stateful
@@ -238,6 +241,28 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain *chains, uint32_t
                          const tlsgpu_record *records, uint32_t nrecords, const uint8_t *pt, uint8_t *wire,
                          tlsgpu_conn_state *states, int32_t *wire_len, uint32_t variant,
                          tlsgpu_event cipher_start, tlsgpu_event cipher_stop);
+
+/* ---- host-buffer seal pipeline: records start and end in host socket buffers
+ * (tlsrecordlayer.py:616-620 writes each sealed record to the socket).  One call
+ * seals a batch whose plaintext arena, descriptors and wire arena are in HOST
+ * memory; connection states stay device-resident.  The batch is cut into
+ * sub-batches of consecutive chains (about chunk_bytes of plaintext each); sub-
+ * batch i's H2D copy, seal and D2H copy run on stream i % depth, so the copies of
+ * one sub-batch overlap the seals of its neighbours.  pt_host / wire_host that
+ * are pinned (tlsgpu_host_alloc) are copied directly; pageable buffers are staged
+ * through library-owned pinned buffers (depth of them per direction, filled and
+ * drained by the calling thread).  Sub-batch copy ranges are cut at the first
+ * record offsets of the next sub-batch, so records should be laid out in chain
+ * order (as tlsgpu_seal_dev callers normally do); any other layout is sealed as
+ * one sub-batch.  Synchronous: wire_host and wire_len_host are complete on return.
+ * wire_len_host: nrecords int32 (as tlsgpu_seal_dev's wire_len). */
+typedef struct tlsgpu_host_pipeline_s *tlsgpu_host_pipeline;
+int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline *p, size_t chunk_bytes, int depth);
+int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p);
+int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain *chains, uint32_t nchains,
+                              const tlsgpu_record *records, uint32_t nrecords, const uint8_t *pt_host,
+                              size_t pt_bytes, uint8_t *wire_host, size_t wire_bytes, tlsgpu_conn_state *states,
+                              int32_t *wire_len_host, uint32_t variant);
 
 /* Batch open: status[r] = plaintext length, or TLSGPU_ALERT_* (records 0..nrecords-1;
  * a chain's records open in order on its state, as successive _decryptRecord calls).

@@ -122,7 +122,7 @@ def test_pipeline_equals_sequential(kind):
     """tlsgpu_pipeline_seal: K successive batches (MAC phase of batch k+1
     overlapping the cipher phase of batch k) give the same wire bytes and final
     connection states as K sequential tlsgpu_seal_dev calls -- for AES, the
-    3DES split path (prefix / MAC / tdes8_kernel) and RC4 + 3DES mixes."""
+    3DES split path (prefix / MAC / tdes4_kernel) and RC4 + 3DES mixes."""
     _T()
     from tlslite_amd import workloads as W
     from tlslite_amd.device import DeviceBuffer, Stream
@@ -279,3 +279,53 @@ def test_unaligned_arenas_vs_oracle(pt_shift, wire_shift, suite, version):
         assert w == ocs[ci].seal(p, ct, fl), (suite, version, len(p), pt_shift, wire_shift)
     for s, o in zip(states, ocs):
         assert s.seqnum == o.seqnum
+
+
+@pytest.mark.parametrize("kind", ["cfg2", "chained", "shuffled"])
+@pytest.mark.parametrize("pinned", [True, False])
+def test_host_pipeline_equals_device_path(kind, pinned):
+    """tlsgpu_host_pipeline_seal (records in host memory; sub-batches' H2D, seal and
+    D2H overlapped on 3 streams, pageable buffers staged through pinned ones) gives
+    the same wire arena, wire lengths and final states as the device-resident
+    tlsgpu_seal_dev path -- with a small chunk so the batch is cut into many
+    sub-batches, and for a shuffled arena layout (one sub-batch)."""
+    _T()
+    from tlslite_amd import workloads as W
+    from tlslite_amd.constants import ContentType
+    from tlslite_amd.device import PinnedBuffer, synchronize
+    from tlslite_amd.recordlayer import HostSealPipeline, make_chains, make_records
+    if kind == "cfg2":
+        wl = W.cfg2(n=700, pt_len=5003, seed=21)
+    elif kind == "chained":
+        wl = W.cfg4(nconn=40, recs_per_conn=5, pt_len=3001, seed=22)
+    else:
+        g = W.cfg2(n=300, pt_len=777, seed=23).groups
+        wl = W.Workload("shuffled", g, 23, rec_order=np.random.default_rng(23).permutation(300))
+    wl.to_device()
+    wl.launch()
+    synchronize()
+    ref_wire, ref_states = wl.d_wire.download(), wl.d_states.download()
+    var = wl.launches[0][0]
+    recs = make_records(wl.pt_off, wl.wire_off, wl.pt_len, ContentType.application_data, 0)
+    chains = make_chains(np.arange(wl.n_chains, dtype=np.uint32), wl.chain_first, wl.chain_count)
+    bufs = []
+    if pinned:
+        bufs = [PinnedBuffer(wl.pt_bytes), PinnedBuffer(wl.wire_bytes)]
+        pt_h, wire_h = bufs[0].array[: wl.pt_bytes], bufs[1].array[: wl.wire_bytes]
+        wire_h[:] = 0
+    else:
+        pt_h, wire_h = np.empty(wl.pt_bytes, dtype=np.uint8), np.zeros(wl.wire_bytes, dtype=np.uint8)
+    wl.d_pt.download(out=pt_h)
+    lens = np.zeros(wl.n_records, dtype=np.int32)
+    wl.reset_states()
+    synchronize()
+    with HostSealPipeline(chunk_bytes=64 << 10, depth=3) as hp:
+        hp.seal(chains, recs, pt_h, wire_h, wl.d_states, lens, var)
+    assert lens.tolist() == wl.wire_len.astype(np.int32).tolist()
+    bad = np.nonzero(wire_h != ref_wire)[0]
+    bad_recs = sorted(set(int(np.searchsorted(wl.wire_off.astype(np.int64), x, side="right")) - 1 for x in bad[:4096]))
+    assert not len(bad), "%d bytes differ, records %s" % (len(bad), bad_recs[:20])
+    assert np.array_equal(wl.d_states.download(), ref_states)
+    for b in bufs:
+        b.free()
+    wl.free()

@@ -98,6 +98,9 @@ SIGNATURES = [
     ("tlsgpu_pipeline_destroy", _i, [_vp]),
     ("tlsgpu_pipeline_synchronize", _i, [_vp]),
     ("tlsgpu_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp]),
+    ("tlsgpu_host_pipeline_create", _i, [ctypes.POINTER(_vp), _sz, _i]),
+    ("tlsgpu_host_pipeline_destroy", _i, [_vp]),
+    ("tlsgpu_host_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _vp, _u32]),
     ("tlsgpu_open_workspace_bytes", _sz, [_u32]),
     ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
     ("tlsgpu_cipher_dev", _i, [_vp, _u32, _vp, _vp, _vp, _i, _i, _vp]),

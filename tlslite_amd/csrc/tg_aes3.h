@@ -13,7 +13,7 @@
 //                  tools/aes_layout_microbench.hip measured best for 256 chains
 //                  per CU.  No barriers: each quad streams its chain: explicit
 //                  IV, full P blocks, then the tail slot.
-//   tdes8_kernel   the 3DES cipher phase (8 lanes per chain).
+//   tdes4_kernel   the 3DES cipher phase (4 lanes per chain).
 //
 // Workspace per record: 32 B meta + 64 B tail slot.  Kernels run in stream
 // order (prefix -> mac -> cbc).  Wave priorities are fixed: the cipher waves
@@ -91,6 +91,9 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_NO_MAC     MAC bulk skipped (wrong MACs; timing of the cipher phase alone)
 //   TG_AB_CBC_NT_ST  ciphertext stores non-temporal
 //   TG_AB_MAC_PRIO / TG_AB_CBC_PRIO  wave priorities of the MAC / cipher waves
+//   TG_AB_MAC_LOADONLY  cooperative MAC: loads + transposes, no compression (timing only)
+//   TG_AB_MAC_NOLOAD    cooperative MAC: compressions on register data, no loads (timing only)
+//   TG_AB_MAC_PF        chunks the cooperative MAC loop prefetches (default 2)
 #ifndef TG_AB_MAC_PRIO
 #define TG_AB_MAC_PRIO 0
 #endif
@@ -133,6 +136,11 @@ __device__ __forceinline__ void mac_bulk(M& mac, const uint8_t* P, uint32_t nful
         mac.update(cur);
     }
 }
+
+#ifndef TG_AB_MAC_PF
+#define TG_AB_MAC_PF 2
+#endif
+constexpr int MAC_PF = TG_AB_MAC_PF;  // chunks prefetched ahead by the cooperative MAC loop
 
 // value of v in lane L of the calling lane's quad
 template <int L>
@@ -179,15 +187,34 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
     NL[L] = quad_lane<L>(nfull) - 1;
     TG_QL(0) TG_QL(1) TG_QL(2) TG_QL(3)
 #undef TG_QL
-    uint4 nxt[4];
+    // prefetch ring of MAC_PF chunks: under the cipher phase's HBM traffic a load takes longer
+    // than one chunk's compression
+    uint4 nxt[MAC_PF][4];
 #pragma unroll
-    for (int L = 0; L < 4; L++) nxt[L] = *(const uint4*)PL[L];
+    for (int d = 0; d < MAC_PF; d++)
+#pragma unroll
+        for (int L = 0; L < 4; L++) {
+#ifdef TG_AB_MAC_NOLOAD
+            nxt[d][L] = make_uint4(lo + L + d, hi, q, L);
+#else
+            nxt[d][L] = *(const uint4*)(PL[L] + 64 * min((uint32_t)d, NL[L]));
+#endif
+        }
     for (uint32_t c = 0; c < nmax; c++) {
         uint4 cur[4];
 #pragma unroll
-        for (int L = 0; L < 4; L++) cur[L] = nxt[L];
+        for (int L = 0; L < 4; L++) cur[L] = nxt[0][L];
 #pragma unroll
-        for (int L = 0; L < 4; L++) nxt[L] = *(const uint4*)(PL[L] + 64 * min(c + 1, NL[L]));
+        for (int d = 0; d + 1 < MAC_PF; d++)
+#pragma unroll
+            for (int L = 0; L < 4; L++) nxt[d][L] = nxt[d + 1][L];
+#ifdef TG_AB_MAC_NOLOAD
+#pragma unroll
+        for (int L = 0; L < 4; L++) nxt[MAC_PF - 1][L] = make_uint4(cur[L].y + c, cur[L].z ^ c, cur[L].w, cur[L].x);
+#else
+#pragma unroll
+        for (int L = 0; L < 4; L++) nxt[MAC_PF - 1][L] = *(const uint4*)(PL[L] + 64 * min(c + MAC_PF, NL[L]));
+#endif
         // component t of lane p's piece of record L = record L's word 4p + t
         uint32_t d[16], x[4];
         x[0] = cur[0].x; x[1] = cur[1].x; x[2] = cur[2].x; x[3] = cur[3].x;
@@ -202,15 +229,24 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
         x[0] = cur[0].w; x[1] = cur[1].w; x[2] = cur[2].w; x[3] = cur[3].w;
         quad_transpose4(x, q);
         d[3] = x[0]; d[7] = x[1]; d[11] = x[2]; d[15] = x[3];
+#ifdef TG_AB_MAC_LOADONLY
+        if (c < nfull) {
+            uint32_t a = 0;
+#pragma unroll
+            for (int i = 0; i < 16; i++) a ^= d[i];
+            mac.h[0] ^= a;
+        }
+#else
         if (c < nfull) mac.update(d);
+#endif
     }
 }
 
 // Register budget: a MAC wave must fit beside four cbc_kernel waves on a SIMD
-// (4 x 96 + 128 <= 512 VGPRs) for the pipeline to overlap the two phases: the launch
-// bound's 4 waves per SIMD caps it at 128.
+// (4 x 80 + 168 <= 512 VGPRs) for the pipeline to overlap the two phases: the launch
+// bound's 3 waves per SIMD caps it at 168.
 template <int MAC, bool SSL3, int BS = 16>
-__global__ void __launch_bounds__(256, 4) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
+__global__ void __launch_bounds__(256, 3) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
                                                  const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
                                                  const ConnState* __restrict__ states, int32_t* __restrict__ wire_len,
                                                  const RecMeta* __restrict__ meta, uint8_t* __restrict__ tails,
@@ -322,12 +358,44 @@ __device__ __forceinline__ void st32t(uint8_t* p, uint32_t v) {
     }
 }
 
-// CBC over nb full plaintext blocks of one chain (P / O include the lane's column offset).
-// Groups of 8 blocks with the next group's columns prefetched; the group loop has no
-// branches and the prefetch index is clamped to the last block (never out of the record),
-// so the compiler's vmcnt waits cover only the loads a block actually consumes -- a
-// conditional load per block made it wait for the whole prefetch (vmcnt(0)) every group.
-// (A per-block prefetch ring pinned with sched_barrier measured 23 % slower on cfg2.)
+// 8 blocks of CBC: take the prefetched column words f (blocks b0..b0+7), refill f with
+// blocks b0+8..b0+15, then encrypt and store the 8 blocks.  CLAMP: the refill index is
+// clamped to the last block (the record's final groups); otherwise the 8 loads are one
+// base address + immediate offsets (fewer VGPRs and no per-block address arithmetic).
+template <int NR, bool AL, bool CLAMP>
+__device__ __forceinline__ uint32_t cbc_group8(const QuadAes& aes, const uint32_t* k, uint32_t iv,
+                                               const uint8_t* P, uint8_t* O, uint32_t b0, uint32_t last,
+                                               uint32_t f[8]) {
+    uint32_t c[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) c[i] = f[i];
+    if constexpr (CLAMP) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t b = b0 + 8 + i;
+            f[i] = ld32t<AL>(P + 16 * (b < last ? b : last));
+        }
+    } else {
+        const uint8_t* Pn = P + 16 * (b0 + 8);
+#pragma unroll
+        for (int i = 0; i < 8; i++) f[i] = ld32t<AL>(Pn + 16 * i);
+    }
+    uint8_t* Ob = O + 16 * b0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(c[i], iv, k[0], 0x96), k);
+        st32t<AL>(Ob + 16 * i, iv);
+    }
+    return iv;
+}
+
+// CBC over nb full plaintext blocks of one chain (P / O include the lane's column offset):
+// groups of 8 blocks with the next group's columns prefetched.  The first group is peeled
+// off the loop: then every path into the loop header ends in the same memory-op pattern
+// (8 loads, 8 stores), and the vmcnt wait the compiler puts at the header only covers the
+// previous group's loads.  With the loop entered straight from the 8 prologue loads, the
+// merged header wait was vmcnt(1) -- every 8 blocks the wave waited for the previous
+// group's stores, which stalls the chain when HBM is loaded (the MAC phase's stream).
 template <int NR, bool AL>
 __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t* k, uint32_t iv,
                                              const uint8_t* P, uint8_t* O, uint32_t nb) {
@@ -337,20 +405,14 @@ __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t*
 #pragma unroll
     for (int i = 0; i < 8; i++) f[i] = ld32t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
     uint32_t b0 = 0;
-    for (; b0 + 8 <= nb; b0 += 8) {
-        uint32_t c[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) c[i] = f[i];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const uint32_t b = b0 + 8 + i;
-            f[i] = ld32t<AL>(P + 16 * (b < last ? b : last));
-        }
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(c[i], iv, k[0], 0x96), k);
-            st32t<AL>(O + 16 * (b0 + i), iv);
-        }
+    if (nb >= 16) {
+        // groups whose refill (blocks b0+8..b0+15) lies inside the record
+        iv = cbc_group8<NR, AL, false>(aes, k, iv, P, O, 0, last, f);
+        for (b0 = 8; b0 + 16 <= nb; b0 += 8) iv = cbc_group8<NR, AL, false>(aes, k, iv, P, O, b0, last, f);
+    }
+    if (b0 + 8 <= nb) {  // the last full group: refill clamped
+        iv = cbc_group8<NR, AL, true>(aes, k, iv, P, O, b0, last, f);
+        b0 += 8;
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -423,62 +485,64 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
 }
 
 // ---------------------------------------------------------------------------
-// tdes8_kernel: 3DES-EDE-CBC (openssl_tripledes.py:23, FIPS 46-3) with 8 lanes per
-// chain.  Lane j of a chain's 8-lane group evaluates ONE of the eight SP-box terms of
-// the Feistel function (a rotate, a key XOR, a 6-bit extract and one conflict-free LDS
-// lookup) and three DPP XOR steps (quad [1,0,3,2], quad [2,3,0,1], half-row mirror) sum
-// the eight terms in every lane of the group, so a round's critical path is one
-// lookup + three XORs instead of one lane issuing all eight lookups and their XOR chain.
-// The (l, r) halves are replicated in the group's lanes; lanes 0/1 store the two
-// ciphertext words.  128 chains per 1024-thread workgroup.  The MAC, the tail slot and
-// the header come from prefix_kernel / mac_kernel<.., 8> as for AES.
-constexpr int D8_THREADS = 1024;
-constexpr int D8_CHAINS = D8_THREADS / 8;
+// tdes4_kernel: 3DES-EDE-CBC (openssl_tripledes.py:23, FIPS 46-3) with 4 lanes per
+// chain.  The Feistel function is eight SP-box lookups, four indexed by the bytes of
+// w = r ^ k_even (tables 7,5,3,1) and four by the bytes of v = rotr4(r) ^ k_odd =
+// rotr4(r ^ rotl4(k_odd)) (tables 6,4,2,0) -- des_rounds().  Lane j of a chain's quad
+// does the two lookups of byte j (one from w, one from v: a rotate, a key XOR, a 6-bit
+// extract and one conflict-free LDS read each), XORs them, and two DPP XOR steps
+// (quad [1,0,3,2], quad [2,3,0,1]) sum the eight terms in every lane of the quad.  A
+// round's critical path is one lookup + three XORs.  Measured against one lookup per lane
+// on 8 lanes (three DPP steps) at cfg5's 128 chains per CU: 6.24 vs 7.25 ms for the
+// cipher alone (tools/des_layout_microbench.hip) -- half the lanes, the same LDS
+// lookups, one DPP step fewer per round.  (l, r) are replicated in the quad; lanes 0/1
+// store the two ciphertext words.  Up to 128 chains per 512-thread workgroup.  The MAC,
+// the tail slot and the header come from prefix_kernel / mac_kernel<.., 8> as for AES.
+constexpr int D4_THREADS = 512;
+constexpr int D4_CHAINS = D4_THREADS / 4;
 
-struct Des8 {
-    uint32_t base, sa;
-    bool odd;
+struct Des4 {
+    uint32_t be, bo, se, so;
     __device__ __forceinline__ void init() {
-        const uint32_t lane = __lane_id(), j = lane & 7;
-        // SP table of each lane: j < 4 take bytes 0..3 of w = r ^ k_even (tables 7,5,3,1),
-        // j >= 4 bytes 0..3 of v = rotr4(r) ^ k_odd = rotr4(r ^ rotl4(k_odd)) (tables 6,4,2,0)
-        // -- des_rounds()
-        const uint32_t K = j < 4 ? 7 - 2 * j : 6 - 2 * (j - 4);
-        base = (lane & 31) * 4 + K * 8192;
-        odd = j >= 4;
-        // rotate so that the lane's 6 index bits (bit (j>=4 ? 4 : 0) + 8*(j&3) of t) land at bits 7..12
-        sa = ((odd ? 4u : 0u) + 8 * (j & 3) + 25u) & 31u;
+        const uint32_t lane = __lane_id(), j = lane & 3;
+        be = (lane & 31) * 4 + (7 - 2 * j) * 8192;
+        bo = (lane & 31) * 4 + (6 - 2 * j) * 8192;
+        // rotate so that the lane's 6 index bits (bit 8j of w, bit 8j+4 of t_odd) land at bits 7..12
+        se = (8 * j + 25u) & 31u;
+        so = (8 * j + 29u) & 31u;
     }
-    // this lane's key word for the SP lookup (odd words pre-rotated, see init)
-    __device__ __forceinline__ uint32_t key(uint32_t even, uint32_t oddw) const {
-        return odd ? ((oddw << 4) | (oddw >> 28)) : even;
-    }
-    // Feistel f of t = r ^ key, summed over the 8 lanes of the group
-    __device__ __forceinline__ uint32_t f(uint32_t t) const {
-        const uint32_t u = __builtin_amdgcn_alignbit(t, t, sa);
-        uint32_t v = lds_read32((u & 0x1f80u) | base);
+    // Feistel f of te = r ^ k_even, to = r ^ rotl4(k_odd), summed over the quad
+    __device__ __forceinline__ uint32_t f(uint32_t te, uint32_t to) const {
+        const uint32_t ue = __builtin_amdgcn_alignbit(te, te, se);
+        const uint32_t uo = __builtin_amdgcn_alignbit(to, to, so);
+        uint32_t v = lds_read32((ue & 0x1f80u) | be) ^ lds_read32((uo & 0x1f80u) | bo);
         v ^= quad_dpp<0xB1>(v);
         v ^= quad_dpp<0x4E>(v);
-        v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false);  // row_half_mirror
         return v;
     }
-    // block as two big-endian words; kw[16p + i] = this lane's key word of pass p, round i.
-    // The next round's t = r' ^ k = l ^ f ^ k is one 3-input XOR off the critical path's f.
-    __device__ __forceinline__ void block(uint32_t& hi, uint32_t& lo, const uint32_t* kw) const {
+    // block as two big-endian words; ke/ko[16p + i] = even / pre-rotated odd key word of
+    // pass p, round i.  The next round's key XORs take l ^ f ^ k in one 3-input XOR each.
+    __device__ __forceinline__ void block(uint32_t& hi, uint32_t& lo, const uint32_t* ke, const uint32_t* ko) const {
         uint32_t l = hi, r = lo;
         des_ip(l, r);
-        uint32_t t = r ^ kw[0];
+        uint32_t te = r ^ ke[0], to = r ^ ko[0];
 #pragma unroll
         for (int g = 0; g < 48; g++) {
-            const uint32_t fv = f(t);
+            const uint32_t fv = f(te, to);
             const uint32_t rn = l ^ fv;
             if (g % 16 != 15) {
-                if (g + 1 < 48) t = __builtin_amdgcn_bitop3_b32(l, fv, kw[g + 1], 0x96);
+                if (g + 1 < 48) {
+                    te = __builtin_amdgcn_bitop3_b32(l, fv, ke[g + 1], 0x96);
+                    to = __builtin_amdgcn_bitop3_b32(l, fv, ko[g + 1], 0x96);
+                }
                 l = r;
                 r = rn;
             } else {  // end of a DES pass: (l, r) = (R16, L16) feeds the next pass
                 l = rn;
-                if (g + 1 < 48) t = r ^ kw[g + 1];
+                if (g + 1 < 48) {
+                    te = r ^ ke[g + 1];
+                    to = r ^ ko[g + 1];
+                }
             }
         }
         des_fp(l, r);
@@ -487,38 +551,40 @@ struct Des8 {
     }
     // CBC on LE words (TdesCbc::enc_block): c = E(p ^ iv), iv = c
     __device__ __forceinline__ void cbc(uint32_t d0, uint32_t d1, uint32_t& iv0, uint32_t& iv1,
-                                        const uint32_t* kw) const {
+                                        const uint32_t* ke, const uint32_t* ko) const {
         uint32_t hi = bswap32(d0 ^ iv0), lo = bswap32(d1 ^ iv1);
-        block(hi, lo, kw);
+        block(hi, lo, ke, ko);
         iv0 = bswap32(hi);
         iv1 = bswap32(lo);
     }
 };
 
-__global__ void __launch_bounds__(D8_THREADS, 1)
-tdes8_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
+__global__ void __launch_bounds__(D4_THREADS, 1)
+tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
              uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
              ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,
              uint32_t cpw, uint32_t epoch) {
-    // SP tables at LDS offset 0 (the kernel's only LDS), read back by absolute address (Des8::f)
-    extern __shared__ __attribute__((aligned(16))) uint32_t d8_lds[];
-    des_lds_fill(d8_lds);
+    // SP tables at LDS offset 0 (the kernel's only LDS), read back by absolute address (Des4::f)
+    extern __shared__ __attribute__((aligned(16))) uint32_t d4_lds[];
+    des_lds_fill(d4_lds);
     __syncthreads();
-    const uint32_t j = threadIdx.x & 7;
-    const uint32_t local = threadIdx.x >> 3;
+    const uint32_t j = threadIdx.x & 3;
+    const uint32_t local = threadIdx.x >> 2;
     const uint32_t cid = blockIdx.x * cpw + local;
-    if (local >= cpw || cid >= nchains) return;  // the 8 lanes of a chain leave together
+    if (local >= cpw || cid >= nchains) return;  // the 4 lanes of a chain leave together
     const tlsgpu_chain ch = chains[cid];
     ConnState* st = states + ch.state;
-    Des8 D;
+    Des4 D;
     D.init();
-    uint32_t kw[48];
+    uint32_t ke[48], ko[48];
 #pragma unroll
     for (int p = 0; p < 3; p++)
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             const int k = p == 1 ? 15 - i : i;  // EDE: the middle pass decrypts (keys backwards)
-            kw[16 * p + i] = D.key(st->des[p][2 * k], st->des[p][2 * k + 1]);
+            const uint32_t od = st->des[p][2 * k + 1];
+            ke[16 * p + i] = st->des[p][2 * k];
+            ko[16 * p + i] = (od << 4) | (od >> 28);
         }
     uint32_t iv0 = st->iv[0], iv1 = st->iv[1];
     const uint32_t f0 = st->fixed_iv[0], f1 = st->fixed_iv[1];
@@ -536,7 +602,7 @@ tdes8_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
         uint8_t* B = wire + R.wire_off + 5;
         const bool al = (((uintptr_t)P | (uintptr_t)B) & 3) == 0;
         if (E) {  // E_K(fixedIVBlock ^ residue) (tlsrecordlayer.py:594-595)
-            D.cbc(f0, f1, iv0, iv1, kw);
+            D.cbc(f0, f1, iv0, iv1, ke, ko);
             if (j < 2) st32(B + 4 * j, j ? iv1 : iv0, al);
         }
         uint8_t* O = B + E;
@@ -547,7 +613,7 @@ tdes8_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
             const uint32_t bn = b + 1 < nb ? b + 1 : b;  // prefetch, clamped to the last block
             n0 = ld32(P + 8 * bn, al);
             n1 = ld32(P + 8 * bn + 4, al);
-            D.cbc(d0, d1, iv0, iv1, kw);
+            D.cbc(d0, d1, iv0, iv1, ke, ko);
             if (j < 2) st32(O + 8 * b + 4 * j, j ? iv1 : iv0, al);
         }
         // tail blocks from the MAC kernel's slot
@@ -555,7 +621,7 @@ tdes8_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
         uint8_t* Ot = O + 8 * nb;
         const uint32_t T = mt.tail_len;
         for (uint32_t off = 0; off < T; off += 8) {
-            D.cbc(*(const uint32_t*)(slot + off), *(const uint32_t*)(slot + off + 4), iv0, iv1, kw);
+            D.cbc(*(const uint32_t*)(slot + off), *(const uint32_t*)(slot + off + 4), iv0, iv1, ke, ko);
             if (j < 2) st32(Ot + off + 4 * j, j ? iv1 : iv0, al);
         }
     }

@@ -7,6 +7,8 @@
 #include <stdio.h>
 #include <map>
 #include <mutex>
+#include <vector>
+#include <stdint.h>
 #include "tg_common.h"
 #include "tg_hash.h"
 #include "tg_keysched.h"
@@ -379,6 +381,245 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain* chains, uint32_t
     if (e != hipSuccess) return fail_hip(e, "pipeline seal");
     TG_HIP(hipEventRecord(p->cbc_done[i], p->cbc_s));
     p->k++;
+    return 0;
+}
+
+// ---------------------------------------------------------------- host-buffer pipeline
+namespace {
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    // zero: clear a fresh allocation (the wire arena: its copy ranges include the alignment
+    // gaps between records, which must not carry stale device memory to the host)
+    hipError_t ensure(size_t need, bool zero = false) {
+        if (bytes >= need && p) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+        }
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, need ? need : 1);
+        if (e == hipSuccess) bytes = need;
+        if (e == hipSuccess && zero) e = hipMemset(p, 0, need ? need : 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+struct PinBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (bytes >= need && p) return hipSuccess;
+        if (p) {
+            hipError_t e = hipHostFree(p);
+            if (e != hipSuccess) return e;
+        }
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipHostMalloc(&p, need ? need : 1, hipHostMallocDefault);
+        if (e == hipSuccess) bytes = need;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    uint8_t* u8() const { return static_cast<uint8_t*>(p); }
+};
+// host memory the DMA engines can read directly (hipHostMalloc / hipHostRegister)
+bool host_pinned(const void* ptr) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+struct SubBatch {
+    uint32_t c0, c1;  // chains [c0, c1)
+    size_t p0, p1;    // plaintext bytes copied H2D
+    size_t w0, w1;    // wire bytes copied D2H
+};
+}  // namespace
+
+struct tlsgpu_host_pipeline_s {
+    int dev = 0;
+    int depth = 2;
+    size_t chunk = 0;
+    std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> done;
+    hipEvent_t ready = nullptr;
+    DevBuf pt, wire, recs, chains, len;
+    std::vector<DevBuf> ws;
+    std::vector<PinBuf> pt_stage, wire_stage;
+};
+
+int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, int depth) {
+    if (!out) return fail(TLSGPU_EINVAL, "null");
+    if (depth < 1 || depth > 16) return fail(TLSGPU_EINVAL, "depth must be 1..16");
+    tlsgpu_host_pipeline p = new tlsgpu_host_pipeline_s();
+    TG_HIP(hipGetDevice(&p->dev));
+    p->depth = depth;
+    p->chunk = chunk_bytes ? chunk_bytes : ((size_t)64 << 20);
+    p->st.resize(depth);
+    p->done.resize(depth);
+    p->ws.resize(depth);
+    p->pt_stage.resize(depth);
+    p->wire_stage.resize(depth);
+    for (int i = 0; i < depth; i++) {
+        TG_HIP(hipStreamCreateWithFlags(&p->st[i], hipStreamNonBlocking));
+        TG_HIP(hipEventCreateWithFlags(&p->done[i], hipEventDisableTiming));
+    }
+    TG_HIP(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
+    *out = p;
+    return 0;
+}
+
+int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p) {
+    if (!p) return 0;
+    for (int i = 0; i < p->depth; i++) (void)hipStreamSynchronize(p->st[i]);
+    p->pt.release();
+    p->wire.release();
+    p->recs.release();
+    p->chains.release();
+    p->len.release();
+    for (int i = 0; i < p->depth; i++) {
+        p->ws[i].release();
+        p->pt_stage[i].release();
+        p->wire_stage[i].release();
+        (void)hipEventDestroy(p->done[i]);
+        (void)hipStreamDestroy(p->st[i]);
+    }
+    (void)hipEventDestroy(p->ready);
+    delete p;
+    return 0;
+}
+
+int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains, uint32_t nchains,
+                              const tlsgpu_record* records, uint32_t nrecords, const uint8_t* pt_host,
+                              size_t pt_bytes, uint8_t* wire_host, size_t wire_bytes, tlsgpu_conn_state* states,
+                              int32_t* wire_len_host, uint32_t variant) {
+    if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
+    if (nchains == 0) return 0;
+    if (!chains || !records || !pt_host || !wire_host || !states || !wire_len_host)
+        return fail(TLSGPU_EINVAL, "null pointer");
+    // sub-batches of consecutive chains, about p->chunk plaintext bytes each
+    std::vector<SubBatch> sub;
+    std::vector<size_t> pmin, wmin, pend, wend;  // per sub-batch extremes over its records
+    {
+        SubBatch cur = {0, 0, 0, 0, 0, 0};
+        size_t acc = 0, lo_p = SIZE_MAX, lo_w = SIZE_MAX, hi_p = 0, hi_w = 0;
+        for (uint32_t c = 0; c < nchains; c++) {
+            const tlsgpu_chain& ch = chains[c];
+            if ((uint64_t)ch.first + ch.count > nrecords) return fail(TLSGPU_EINVAL, "chain outside the records");
+            for (uint32_t k = 0; k < ch.count; k++) {
+                const tlsgpu_record& R = records[ch.first + k];
+                if (R.pt_off + R.pt_len > pt_bytes || R.wire_off + 5 + (uint64_t)R.pt_len > wire_bytes)
+                    return fail(TLSGPU_EINVAL, "record outside the host arenas");
+                lo_p = R.pt_off < lo_p ? R.pt_off : lo_p;
+                lo_w = R.wire_off < lo_w ? R.wire_off : lo_w;
+                hi_p = R.pt_off + R.pt_len > hi_p ? R.pt_off + R.pt_len : hi_p;
+                hi_w = R.wire_off + 5 + R.pt_len > hi_w ? R.wire_off + 5 + R.pt_len : hi_w;
+                acc += R.pt_len;
+            }
+            cur.c1 = c + 1;
+            if (acc >= p->chunk || c + 1 == nchains) {
+                sub.push_back(cur);
+                pmin.push_back(lo_p == SIZE_MAX ? 0 : lo_p);
+                wmin.push_back(lo_w == SIZE_MAX ? 0 : lo_w);
+                pend.push_back(hi_p);
+                wend.push_back(hi_w);
+                cur.c0 = c + 1;
+                acc = 0;
+                lo_p = lo_w = SIZE_MAX;
+                hi_p = hi_w = 0;
+            }
+        }
+        // copy ranges: from this sub-batch's first offset to the next one's; a layout that is
+        // not monotone in chain order (ranges would overlap) is sealed as one sub-batch
+        bool mono = true;
+        for (size_t i = 0; i + 1 < sub.size(); i++)
+            if (pend[i] > pmin[i + 1] || wend[i] > wmin[i + 1] || pmin[i + 1] < pmin[i] || wmin[i + 1] < wmin[i])
+                mono = false;
+        if (!mono) {
+            sub.assign(1, SubBatch{0, nchains, 0, 0, 0, 0});
+            pmin.assign(1, 0);
+            wmin.assign(1, 0);
+        }
+        for (size_t i = 0; i < sub.size(); i++) {
+            sub[i].p0 = mono ? pmin[i] : 0;
+            sub[i].w0 = mono ? wmin[i] : 0;
+            sub[i].p1 = (mono && i + 1 < sub.size()) ? pmin[i + 1] : pt_bytes;
+            sub[i].w1 = (mono && i + 1 < sub.size()) ? wmin[i + 1] : wire_bytes;
+        }
+    }
+    const int D = p->depth;
+    const bool pt_direct = host_pinned(pt_host), wire_direct = host_pinned(wire_host);
+    size_t max_p = 0, max_w = 0;
+    for (const SubBatch& b : sub) {
+        max_p = b.p1 - b.p0 > max_p ? b.p1 - b.p0 : max_p;
+        max_w = b.w1 - b.w0 > max_w ? b.w1 - b.w0 : max_w;
+    }
+    TG_HIP(p->pt.ensure(pt_bytes));
+    TG_HIP(p->wire.ensure(wire_bytes, true));
+    TG_HIP(p->recs.ensure((size_t)nrecords * sizeof(tlsgpu_record)));
+    TG_HIP(p->chains.ensure((size_t)nchains * sizeof(tlsgpu_chain)));
+    TG_HIP(p->len.ensure((size_t)nrecords * 4));
+    const bool need_ws = seal_needs_workspace(variant);
+    for (int i = 0; i < D; i++) {
+        if (need_ws) TG_HIP(p->ws[i].ensure(seal_workspace_bytes(nrecords)));
+        if (!pt_direct) TG_HIP(p->pt_stage[i].ensure(max_p));
+        if (!wire_direct) TG_HIP(p->wire_stage[i].ensure(max_w));
+    }
+    // descriptors once (small), every stream ordered after them
+    TG_HIP(hipMemcpyAsync(p->recs.p, records, (size_t)nrecords * sizeof(tlsgpu_record), hipMemcpyHostToDevice, p->st[0]));
+    TG_HIP(hipMemcpyAsync(p->chains.p, chains, (size_t)nchains * sizeof(tlsgpu_chain), hipMemcpyHostToDevice, p->st[0]));
+    TG_HIP(hipEventRecord(p->ready, p->st[0]));
+    for (int i = 1; i < D; i++) TG_HIP(hipStreamWaitEvent(p->st[i], p->ready, 0));
+    const tlsgpu_chain* d_chains = static_cast<const tlsgpu_chain*>(p->chains.p);
+    const tlsgpu_record* d_recs = static_cast<const tlsgpu_record*>(p->recs.p);
+    // finish sub-batch j's D2H staging copy (CPU) once its stream has drained it
+    auto drain = [&](size_t j) -> int {
+        const int t = (int)(j % D);
+        TG_HIP(hipEventSynchronize(p->done[t]));
+        if (!wire_direct) memcpy(wire_host + sub[j].w0, p->wire_stage[t].u8(), sub[j].w1 - sub[j].w0);
+        return 0;
+    };
+    for (size_t i = 0; i < sub.size(); i++) {
+        const SubBatch& b = sub[i];
+        const int t = (int)(i % D);
+        hipStream_t s = p->st[t];
+        if (i >= (size_t)D) {
+            int rc = drain(i - D);
+            if (rc) return rc;
+        }
+        const uint8_t* src = pt_host + b.p0;
+        if (!pt_direct) {
+            memcpy(p->pt_stage[t].u8(), src, b.p1 - b.p0);
+            src = p->pt_stage[t].u8();
+        }
+        if (b.p1 > b.p0) TG_HIP(hipMemcpyAsync(p->pt.u8() + b.p0, src, b.p1 - b.p0, hipMemcpyHostToDevice, s));
+        bool known = false;
+        hipError_t e = launch_seal(variant, d_chains + b.c0, b.c1 - b.c0, d_recs, nrecords, p->pt.u8(), p->wire.u8(),
+                                   S(states), static_cast<int32_t*>(p->len.p), p->ws[t].u8(), next_epoch(), s, &known);
+        if (!known) return fail(TLSGPU_EINVAL, "unsupported seal variant");
+        if (e != hipSuccess) return fail_hip(e, "host pipeline seal");
+        uint8_t* dst = wire_direct ? wire_host + b.w0 : p->wire_stage[t].u8();
+        if (b.w1 > b.w0) TG_HIP(hipMemcpyAsync(dst, p->wire.u8() + b.w0, b.w1 - b.w0, hipMemcpyDeviceToHost, s));
+        TG_HIP(hipEventRecord(p->done[t], s));
+    }
+    for (size_t j = sub.size() > (size_t)D ? sub.size() - D : 0; j < sub.size(); j++) {
+        int rc = drain(j);
+        if (rc) return rc;
+    }
+    TG_HIP(hipMemcpy(wire_len_host, p->len.p, (size_t)nrecords * 4, hipMemcpyDeviceToHost));
     return 0;
 }
 

@@ -1,5 +1,5 @@
 // tg_kernels.hip -- gfx950 kernels of libtlsgpu.so and their launchers:
-//   prefix/mac/cbc_kernel, tdes8_kernel   split AES / 3DES seal (tg_aes3.h)
+//   prefix/mac/cbc_kernel, tdes4_kernel   split AES / 3DES seal (tg_aes3.h)
 //   rc4_seal_kernel  fused per-record MAC -> RC4 -> header, one lane per connection
 //                    chain (tlsrecordlayer.py:538-617, python_rc4.py:25-41)
 //   open_*_kernel    AES open (tg_open3.h); open_kernel: RC4 / 3DES open, lane per chain
@@ -420,10 +420,10 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
     if constexpr (NR == 0) {  // 3DES: 8 lanes per chain
         uint32_t pw = (nchains + ncu - 1) / ncu;
-        pw = pw < 1 ? 1 : (pw > (uint32_t)D8_CHAINS ? (uint32_t)D8_CHAINS : pw);
-        hipError_t e = set_lds(tdes8_kernel, DES_LDS_BYTES);
+        pw = pw < 1 ? 1 : (pw > (uint32_t)D4_CHAINS ? (uint32_t)D4_CHAINS : pw);
+        hipError_t e = set_lds(tdes4_kernel, DES_LDS_BYTES);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(tdes8_kernel, dim3((nchains + pw - 1) / pw), dim3(D8_THREADS), DES_LDS_BYTES, s, chains,
+        hipLaunchKernelGGL(tdes4_kernel, dim3((nchains + pw - 1) / pw), dim3(D4_THREADS), DES_LDS_BYTES, s, chains,
                            nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch);
         return hipGetLastError();
     } else {

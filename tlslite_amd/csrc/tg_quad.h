@@ -17,11 +17,13 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
 
 __device__ __forceinline__ uint32_t lds_read32(uint32_t addr) { return *(const lds_u32_t*)(size_t)addr; }
 
-// v_xor_b32_dpp-able quad permutation (update_dpp with old=0 lets the DPP
-// combiner fold the move into the consuming XOR)
+// v_xor_b32_dpp-able quad permutation.  bound_ctrl set: every lane of a quad_perm reads
+// an in-range lane, so the "old" operand is never used and the compiler needs no zeroed
+// destination register for an unfolded v_mov_b32_dpp (it kept 16 of them live in the
+// cipher loop, plus a v_mov each, when the final round's masks blocked the fold).
 template <int CTRL>
 __device__ __forceinline__ uint32_t quad_dpp(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
 }
 
 struct QuadAes {

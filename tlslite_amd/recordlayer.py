@@ -160,6 +160,39 @@ class SealPipeline:
         self.close()
 
 
+class HostSealPipeline:
+    """Seal batches whose plaintext and wire arenas live in HOST memory
+    (tlsgpu_host_pipeline_*): the records' socket-buffer hand-off
+    (tlsrecordlayer.py:616-620) with H2D copy, seal and D2H copy of successive
+    sub-batches overlapped on `depth` streams.  Pinned host arrays
+    (device.PinnedBuffer) are copied directly, pageable ones through
+    library-owned pinned staging buffers."""
+
+    def __init__(self, chunk_bytes=64 << 20, depth=3):
+        h = ctypes.c_void_p()
+        N.call("tlsgpu_host_pipeline_create", ctypes.byref(h), int(chunk_bytes), int(depth))
+        self.handle = h
+
+    def seal(self, chains, records, pt_host, wire_host, states, wire_len_host, variant):
+        """chains / records: ctypes arrays (host); pt_host / wire_host: numpy uint8
+        arrays (host); states: DeviceBuffer; wire_len_host: numpy int32 [nrecords]."""
+        N.call("tlsgpu_host_pipeline_seal", self.handle, ctypes.addressof(chains), len(chains),
+               ctypes.addressof(records), len(records), pt_host.ctypes.data_as(ctypes.c_void_p), pt_host.nbytes,
+               wire_host.ctypes.data_as(ctypes.c_void_p), wire_host.nbytes, states.ptr,
+               wire_len_host.ctypes.data_as(ctypes.c_void_p), variant)
+
+    def close(self):
+        if self.handle is not None and self.handle.value:
+            N.call("tlsgpu_host_pipeline_destroy", self.handle)
+        self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 def seal(states, records, stream=None, pt_shift=0, wire_shift=0):
     """Seal records on the GPU.
 

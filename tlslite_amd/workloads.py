@@ -264,8 +264,8 @@ class Workload:
             return "cbc_kernel<%d>" % (10 if c == N.CIPHER_AES128 else 14)
         if c == N.CIPHER_3DES:
             # split path: bench.py's events bracket the whole 3DES seal call (prefix + MAC +
-            # tdes8_kernel), which tdes8_kernel dominates
-            return "tdes8_kernel"
+            # tdes4_kernel), which tdes4_kernel dominates
+            return "tdes4_kernel"
         return "rc4_seal_kernel"
 
     def aes_lookups(self):
