@@ -148,10 +148,52 @@ def oracle_check(wl, wire_gpu, nthreads, sample=None, min_seconds=0.0):
 PCIE_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s per direction (spec)
 
 
-def host_inclusive_rate(wl, chunk=32 << 20, depth=3):
+def pcie_rates(nbytes=256 << 20):
+    """Measured pinned copy rates on this box with the HIP runtime directly (ctypes on
+    libamdhip64, the engines the host pipeline uses): H2D alone, D2H alone, and both
+    at once on two streams (GB/s; the last is the total of both directions).  Same
+    method as tools/pcie_probe.hip."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    vp = ctypes.c_void_p
+    h1, h2, d1, d2, s1, s2 = vp(), vp(), vp(), vp(), vp(), vp()
+    for ptr in (h1, h2):
+        if hip.hipHostMalloc(ctypes.byref(ptr), ctypes.c_size_t(nbytes), 0):
+            return None
+    for ptr in (d1, d2):
+        if hip.hipMalloc(ctypes.byref(ptr), ctypes.c_size_t(nbytes)):
+            return None
+    hip.hipStreamCreateWithFlags(ctypes.byref(s1), 1)
+    hip.hipStreamCreateWithFlags(ctypes.byref(s2), 1)
+    hip.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
+    res = {}
+    for name, mode in (("h2d", 1), ("d2h", 2), ("both", 3)):
+        best = None
+        for _ in range(4):
+            hip.hipDeviceSynchronize()
+            t0 = time.perf_counter()
+            if mode & 1:
+                hip.hipMemcpyAsync(d1, h1, nbytes, 1, s1)
+            if mode & 2:
+                hip.hipMemcpyAsync(h2, d2, nbytes, 2, s2)
+            hip.hipStreamSynchronize(s1)
+            hip.hipStreamSynchronize(s2)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        res[name] = round(nbytes * (2 if mode == 3 else 1) / best / 1e9, 1)
+    for ptr in (h1, h2):
+        hip.hipHostFree(ptr)
+    for ptr in (d1, d2):
+        hip.hipFree(ptr)
+    hip.hipStreamDestroy(s1)
+    hip.hipStreamDestroy(s2)
+    return res
+
+
+def host_inclusive_rate(wl, chunk=64 << 20, depth=3):
     """Plaintext GiB/s with the records starting and ending in HOST memory, through the
     C host pipeline (tlsgpu_host_pipeline_seal: H2D of plaintext, seal, D2H of the
-    wire arena, sub-batches overlapped on `depth` streams), for pinned host arenas and
+    wire arena per sub-batch on three streams, `depth` sub-batches in flight), for pinned host arenas and
     for pageable ones (staged through the library's pinned buffers).  The wire output
     of both is compared with the device-resident path's.  Never `value`."""
     from tlslite_amd import _native as N
@@ -172,12 +214,23 @@ def host_inclusive_rate(wl, chunk=32 << 20, depth=3):
     wl.d_pt.download(out=pin_pt.array[: wl.pt_bytes])
     pag_pt, pag_wire = pin_pt.array[: wl.pt_bytes].copy(), np.zeros(wl.wire_bytes, dtype=np.uint8)
     lens = np.zeros(wl.n_records, dtype=np.int32)
+    link = pcie_rates()
+    if link:
+        # both directions at once share the link: the copies need at least
+        # max(H2D bytes / H2D rate, D2H bytes / D2H rate, all bytes / both-at-once rate)
+        t_min = max(wl.pt_bytes / (link["h2d"] * 1e9), wl.wire_bytes / (link["d2h"] * 1e9),
+                    (wl.pt_bytes + wl.wire_bytes) / (link["both"] * 1e9))
+        how = "measured pinned hipMemcpyAsync rates on this box (pcie_measured_gbs)"
+    else:
+        t_min = max(wl.pt_bytes, wl.wire_bytes) / (PCIE_GBS * 1e9)
+        how = "63 GB/s per direction, full duplex (spec)"
     out = {"unit": "GiB/s", "chunk_bytes": chunk, "depth": depth,
            "bytes_h2d": int(wl.pt_bytes), "bytes_d2h": int(wl.wire_bytes),
-           "pcie_ceiling": round(wl.plaintext_total / GIB / (max(wl.pt_bytes, wl.wire_bytes) / (PCIE_GBS * 1e9)), 2),
+           "pcie_measured_gbs": link,
+           "pcie_ceiling": round(wl.plaintext_total / GIB / t_min, 2),
            "method": "tlsgpu_host_pipeline_seal: per sub-batch of ~chunk_bytes plaintext H2D copy, seal, D2H copy "
-                     "of its wire range, sub-batches on `depth` streams; wall time of the synchronous call, best of 3; "
-                     "pcie_ceiling = plaintext / (max(H2D, D2H bytes) at 63 GB/s per direction, full duplex)"}
+                     "of its wire range on three streams (one per engine), `depth` sub-batches in flight; wall time of "
+                     "the synchronous call, best of 3; pcie_ceiling = plaintext / the copies' minimum time at " + how}
     with HostSealPipeline(chunk, depth) as hp:
         for name, pt_h, wire_h in (("pinned", pin_pt.array[: wl.pt_bytes], pin_wire.array[: wl.wire_bytes]),
                                    ("pageable", pag_pt, pag_wire)):

@@ -230,7 +230,8 @@ int tlsgpu_seal_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_r
                     tlsgpu_stream s);
 /* ---- seal pipeline: successive tlsgpu_pipeline_seal calls overlap the MAC
  * phase of call k+1 with the cipher phase of call k (AES suites; two
- * library-owned streams, double-buffered workspace).  Inputs must be ready
+ * library-owned streams, three workspaces in rotation, so the MAC phase may run
+ * up to two calls ahead).  Inputs must be ready
  * when a call is made and stay valid, and outputs are complete, only after
  * tlsgpu_pipeline_synchronize.  Optional events bracket the cipher kernel. */
 typedef struct tlsgpu_pipeline_s *tlsgpu_pipeline;
@@ -246,9 +247,11 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain *chains, uint32_t
  * (tlsrecordlayer.py:616-620 writes each sealed record to the socket).  One call
  * seals a batch whose plaintext arena, descriptors and wire arena are in HOST
  * memory; connection states stay device-resident.  The batch is cut into
- * sub-batches of consecutive chains (about chunk_bytes of plaintext each); sub-
- * batch i's H2D copy, seal and D2H copy run on stream i % depth, so the copies of
- * one sub-batch overlap the seals of its neighbours.  pt_host / wire_host that
+ * sub-batches of consecutive chains (about chunk_bytes of plaintext each).  Four
+ * library-owned streams chained per sub-batch by events: H2D copies of the sub-batches'
+ * plaintext, their MAC phases, their cipher phases, D2H copies of their wire ranges --
+ * so copies in both directions, the MAC phase of one sub-batch and the cipher phase of
+ * the one before run at once; `depth` sub-batches are in flight.  pt_host / wire_host that
  * are pinned (tlsgpu_host_alloc) are copied directly; pageable buffers are staged
  * through library-owned pinned buffers (depth of them per direction, filled and
  * drained by the calling thread).  Sub-batch copy ranges are cut at the first

@@ -303,11 +303,17 @@ int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_r
 }
 
 // ---------------------------------------------------------------- pipeline
+// Workspaces in rotation: the MAC phase of call k reuses the workspace of call k - PIPE_WS,
+// so the MAC stream may run up to PIPE_WS - 1 calls ahead of the cipher stream.
+#ifndef TG_AB_PIPE_WS
+#define TG_AB_PIPE_WS 3
+#endif
+constexpr int PIPE_WS = TG_AB_PIPE_WS;
 struct tlsgpu_pipeline_s {
     int dev;
     hipStream_t mac_s, cbc_s;
-    hipEvent_t mac_done[2], cbc_done[2];
-    void* ws[2];
+    hipEvent_t mac_done[PIPE_WS], cbc_done[PIPE_WS];
+    void* ws[PIPE_WS];
     size_t ws_bytes;
     uint64_t k;
 };
@@ -318,12 +324,12 @@ int tlsgpu_pipeline_create(tlsgpu_pipeline* out, uint32_t max_records) {
     TG_HIP(hipGetDevice(&p->dev));
     TG_HIP(hipStreamCreateWithFlags(&p->mac_s, hipStreamNonBlocking));
     TG_HIP(hipStreamCreateWithFlags(&p->cbc_s, hipStreamNonBlocking));
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < PIPE_WS; i++) {
         TG_HIP(hipEventCreateWithFlags(&p->mac_done[i], hipEventDisableTiming));
         TG_HIP(hipEventCreateWithFlags(&p->cbc_done[i], hipEventDisableTiming));
     }
     p->ws_bytes = seal_workspace_bytes(max_records ? max_records : 1);
-    for (int i = 0; i < 2; i++) TG_HIP(hipMalloc(&p->ws[i], p->ws_bytes));
+    for (int i = 0; i < PIPE_WS; i++) TG_HIP(hipMalloc(&p->ws[i], p->ws_bytes));
     p->k = 0;
     *out = p;
     return 0;
@@ -333,7 +339,7 @@ int tlsgpu_pipeline_destroy(tlsgpu_pipeline p) {
     if (!p) return 0;
     (void)hipStreamSynchronize(p->mac_s);
     (void)hipStreamSynchronize(p->cbc_s);
-    for (int i = 0; i < 2; i++) {
+    for (int i = 0; i < PIPE_WS; i++) {
         (void)hipFree(p->ws[i]);
         (void)hipEventDestroy(p->mac_done[i]);
         (void)hipEventDestroy(p->cbc_done[i]);
@@ -360,9 +366,9 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain* chains, uint32_t
     if (seal_workspace_bytes(nrecords) > p->ws_bytes) return fail(TLSGPU_EINVAL, "nrecords > pipeline max_records");
     static uint32_t epoch_ctr = 0x80000000u;
     const uint32_t epoch = __atomic_add_fetch(&epoch_ctr, 1, __ATOMIC_RELAXED);
-    const int i = (int)(p->k & 1);
-    // workspace i was last read by the cipher phase of call k-2
-    if (p->k >= 2) TG_HIP(hipStreamWaitEvent(p->mac_s, p->cbc_done[i], 0));
+    const int i = (int)(p->k % PIPE_WS);
+    // workspace i was last read by the cipher phase of call k - PIPE_WS
+    if (p->k >= (uint64_t)PIPE_WS) TG_HIP(hipStreamWaitEvent(p->mac_s, p->cbc_done[i], 0));
     bool known = false;
     hipError_t e = hipSuccess;
     if (seal_needs_workspace(variant)) {
@@ -449,13 +455,25 @@ struct SubBatch {
 };
 }  // namespace
 
+// Four streams, chained per sub-batch by events: h2d (plaintext copies) and d2h (wire
+// copies), one per copy direction so both directions run at once (pinned: 57 GB/s each
+// way, 97 GB/s both at once on the MI355X box, tools/pcie_probe.hip), and the seal's
+// two phases on mac (prefix + MAC kernels) and cbc (cipher kernel), so the MAC phase of
+// sub-batch i+1 runs beside the cipher phase of sub-batch i as in tlsgpu_pipeline_seal.
+// A sub-batch of a few thousand single-record chains is a latency-bound seal (~0.4 ms
+// MAC + ~0.5 ms CBC for 16 KiB records whatever the chain count up to ~64 per CU), so
+// the phases must overlap for the seals to keep up with the copies.  Separate streams
+// per kernel kind, not per slot: the runtime spreads streams over only a few hardware
+// queues, and kernels of streams that share a queue run in submission order.
+// `depth` sub-batches are in flight: slot i % depth's staging buffers and workspace are
+// reused once sub-batch i - depth is done.
 struct tlsgpu_host_pipeline_s {
     int dev = 0;
     int depth = 2;
     size_t chunk = 0;
-    std::vector<hipStream_t> st;
-    std::vector<hipEvent_t> done;
-    hipEvent_t ready = nullptr;
+    hipStream_t h2d = nullptr, mac = nullptr, cbc = nullptr, d2h = nullptr;
+    std::vector<hipEvent_t> mac_done;
+    std::vector<hipEvent_t> in_done, seal_done, out_done;
     DevBuf pt, wire, recs, chains, len;
     std::vector<DevBuf> ws;
     std::vector<PinBuf> pt_stage, wire_stage;
@@ -468,23 +486,36 @@ int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, i
     TG_HIP(hipGetDevice(&p->dev));
     p->depth = depth;
     p->chunk = chunk_bytes ? chunk_bytes : ((size_t)64 << 20);
-    p->st.resize(depth);
-    p->done.resize(depth);
+    p->in_done.resize(depth);
+    p->seal_done.resize(depth);
+    p->out_done.resize(depth);
     p->ws.resize(depth);
     p->pt_stage.resize(depth);
     p->wire_stage.resize(depth);
+    p->mac_done.resize(depth);
+    // The runtime spreads streams over a few hardware queues per priority, and a copy holds
+    // its queue until it completes (kernels queued behind it wait; with the MAC stream
+    // behind the H2D copies on one queue the call took 31.9 instead of 24.6 ms): the copy
+    // streams are created at high priority, away from the kernel streams' queues.
+    int lo_prio = 0, hi_prio = 0;
+    TG_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+    TG_HIP(hipStreamCreateWithPriority(&p->h2d, hipStreamNonBlocking, hi_prio));
+    TG_HIP(hipStreamCreateWithPriority(&p->d2h, hipStreamNonBlocking, hi_prio));
+    TG_HIP(hipStreamCreateWithFlags(&p->mac, hipStreamNonBlocking));
+    TG_HIP(hipStreamCreateWithFlags(&p->cbc, hipStreamNonBlocking));
     for (int i = 0; i < depth; i++) {
-        TG_HIP(hipStreamCreateWithFlags(&p->st[i], hipStreamNonBlocking));
-        TG_HIP(hipEventCreateWithFlags(&p->done[i], hipEventDisableTiming));
+        TG_HIP(hipEventCreateWithFlags(&p->mac_done[i], hipEventDisableTiming));
+        TG_HIP(hipEventCreateWithFlags(&p->in_done[i], hipEventDisableTiming));
+        TG_HIP(hipEventCreateWithFlags(&p->seal_done[i], hipEventDisableTiming));
+        TG_HIP(hipEventCreateWithFlags(&p->out_done[i], hipEventDisableTiming));
     }
-    TG_HIP(hipEventCreateWithFlags(&p->ready, hipEventDisableTiming));
     *out = p;
     return 0;
 }
 
 int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p) {
     if (!p) return 0;
-    for (int i = 0; i < p->depth; i++) (void)hipStreamSynchronize(p->st[i]);
+    for (hipStream_t s : {p->h2d, p->mac, p->cbc, p->d2h}) (void)hipStreamSynchronize(s);
     p->pt.release();
     p->wire.release();
     p->recs.release();
@@ -494,10 +525,12 @@ int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p) {
         p->ws[i].release();
         p->pt_stage[i].release();
         p->wire_stage[i].release();
-        (void)hipEventDestroy(p->done[i]);
-        (void)hipStreamDestroy(p->st[i]);
+        (void)hipEventDestroy(p->in_done[i]);
+        (void)hipEventDestroy(p->seal_done[i]);
+        (void)hipEventDestroy(p->out_done[i]);
+        (void)hipEventDestroy(p->mac_done[i]);
     }
-    (void)hipEventDestroy(p->ready);
+    for (hipStream_t s : {p->h2d, p->mac, p->cbc, p->d2h}) (void)hipStreamDestroy(s);
     delete p;
     return 0;
 }
@@ -578,47 +611,69 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
         if (!pt_direct) TG_HIP(p->pt_stage[i].ensure(max_p));
         if (!wire_direct) TG_HIP(p->wire_stage[i].ensure(max_w));
     }
-    // descriptors once (small), every stream ordered after them
-    TG_HIP(hipMemcpyAsync(p->recs.p, records, (size_t)nrecords * sizeof(tlsgpu_record), hipMemcpyHostToDevice, p->st[0]));
-    TG_HIP(hipMemcpyAsync(p->chains.p, chains, (size_t)nchains * sizeof(tlsgpu_chain), hipMemcpyHostToDevice, p->st[0]));
-    TG_HIP(hipEventRecord(p->ready, p->st[0]));
-    for (int i = 1; i < D; i++) TG_HIP(hipStreamWaitEvent(p->st[i], p->ready, 0));
+    // descriptors once (small), on the h2d stream ahead of the first sub-batch's plaintext
+    TG_HIP(hipMemcpyAsync(p->recs.p, records, (size_t)nrecords * sizeof(tlsgpu_record), hipMemcpyHostToDevice, p->h2d));
+    TG_HIP(hipMemcpyAsync(p->chains.p, chains, (size_t)nchains * sizeof(tlsgpu_chain), hipMemcpyHostToDevice, p->h2d));
     const tlsgpu_chain* d_chains = static_cast<const tlsgpu_chain*>(p->chains.p);
     const tlsgpu_record* d_recs = static_cast<const tlsgpu_record*>(p->recs.p);
-    // finish sub-batch j's D2H staging copy (CPU) once its stream has drained it
+    // finish sub-batch j (CPU): wait for its D2H copy, then unstage it
     auto drain = [&](size_t j) -> int {
         const int t = (int)(j % D);
-        TG_HIP(hipEventSynchronize(p->done[t]));
+        TG_HIP(hipEventSynchronize(p->out_done[t]));
         if (!wire_direct) memcpy(wire_host + sub[j].w0, p->wire_stage[t].u8(), sub[j].w1 - sub[j].w0);
         return 0;
     };
+    // Pinned arenas: everything is enqueued at once and ordered on the GPU (slot t's seal
+    // stream keeps its workspace in order), the calling thread only waits at the end.
+    // Staged arenas: before refilling slot t's plaintext stage the thread waits for the
+    // H2D copy of sub-batch i - D, and before enqueueing the D2H copy into slot t's wire
+    // stage it unstages sub-batch i - D.
     for (size_t i = 0; i < sub.size(); i++) {
         const SubBatch& b = sub[i];
         const int t = (int)(i % D);
-        hipStream_t s = p->st[t];
-        if (i >= (size_t)D) {
-            int rc = drain(i - D);
-            if (rc) return rc;
-        }
         const uint8_t* src = pt_host + b.p0;
         if (!pt_direct) {
+            if (i >= (size_t)D) TG_HIP(hipEventSynchronize(p->in_done[t]));
             memcpy(p->pt_stage[t].u8(), src, b.p1 - b.p0);
             src = p->pt_stage[t].u8();
         }
-        if (b.p1 > b.p0) TG_HIP(hipMemcpyAsync(p->pt.u8() + b.p0, src, b.p1 - b.p0, hipMemcpyHostToDevice, s));
+        if (b.p1 > b.p0) TG_HIP(hipMemcpyAsync(p->pt.u8() + b.p0, src, b.p1 - b.p0, hipMemcpyHostToDevice, p->h2d));
+        TG_HIP(hipEventRecord(p->in_done[t], p->h2d));
+        TG_HIP(hipStreamWaitEvent(p->mac, p->in_done[t], 0));
+        // slot t's workspace: the cipher phase of sub-batch i - D has read it
+        if (i >= (size_t)D) TG_HIP(hipStreamWaitEvent(p->mac, p->seal_done[t], 0));
         bool known = false;
-        hipError_t e = launch_seal(variant, d_chains + b.c0, b.c1 - b.c0, d_recs, nrecords, p->pt.u8(), p->wire.u8(),
-                                   S(states), static_cast<int32_t*>(p->len.p), p->ws[t].u8(), next_epoch(), s, &known);
+        hipError_t e;
+        if (need_ws) {
+            e = launch_seal_phases(variant, d_chains + b.c0, b.c1 - b.c0, d_recs, nrecords, p->pt.u8(), p->wire.u8(),
+                                   S(states), static_cast<int32_t*>(p->len.p), p->ws[t].u8(), next_epoch(), p->mac,
+                                   p->mac_done[t], p->cbc, nullptr, nullptr, &known);
+        } else {  // single-kernel variants (RC4) on the cipher stream
+            TG_HIP(hipStreamWaitEvent(p->cbc, p->in_done[t], 0));
+            e = launch_seal(variant, d_chains + b.c0, b.c1 - b.c0, d_recs, nrecords, p->pt.u8(), p->wire.u8(),
+                            S(states), static_cast<int32_t*>(p->len.p), nullptr, next_epoch(), p->cbc, &known);
+        }
         if (!known) return fail(TLSGPU_EINVAL, "unsupported seal variant");
         if (e != hipSuccess) return fail_hip(e, "host pipeline seal");
+        TG_HIP(hipEventRecord(p->seal_done[t], p->cbc));
+        if (!wire_direct && i >= (size_t)D) {
+            int rc = drain(i - D);
+            if (rc) return rc;
+        }
+        TG_HIP(hipStreamWaitEvent(p->d2h, p->seal_done[t], 0));
         uint8_t* dst = wire_direct ? wire_host + b.w0 : p->wire_stage[t].u8();
-        if (b.w1 > b.w0) TG_HIP(hipMemcpyAsync(dst, p->wire.u8() + b.w0, b.w1 - b.w0, hipMemcpyDeviceToHost, s));
-        TG_HIP(hipEventRecord(p->done[t], s));
+        if (b.w1 > b.w0) TG_HIP(hipMemcpyAsync(dst, p->wire.u8() + b.w0, b.w1 - b.w0, hipMemcpyDeviceToHost, p->d2h));
+        TG_HIP(hipEventRecord(p->out_done[t], p->d2h));
     }
-    for (size_t j = sub.size() > (size_t)D ? sub.size() - D : 0; j < sub.size(); j++) {
-        int rc = drain(j);
-        if (rc) return rc;
+    if (wire_direct) {
+        TG_HIP(hipStreamSynchronize(p->d2h));
+    } else {
+        for (size_t j = sub.size() > (size_t)D ? sub.size() - D : 0; j < sub.size(); j++) {
+            int rc = drain(j);
+            if (rc) return rc;
+        }
     }
+    // wire_len: ordered after every seal (each seal_done precedes its D2H copy, all drained)
     TG_HIP(hipMemcpy(wire_len_host, p->len.p, (size_t)nrecords * 4, hipMemcpyDeviceToHost));
     return 0;
 }

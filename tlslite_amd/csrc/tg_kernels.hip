@@ -418,7 +418,7 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
     const uint32_t ncu = cu_count();
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
-    if constexpr (NR == 0) {  // 3DES: 8 lanes per chain
+    if constexpr (NR == 0) {  // 3DES: 4 lanes per chain
         uint32_t pw = (nchains + ncu - 1) / ncu;
         pw = pw < 1 ? 1 : (pw > (uint32_t)D4_CHAINS ? (uint32_t)D4_CHAINS : pw);
         hipError_t e = set_lds(tdes4_kernel, DES_LDS_BYTES);

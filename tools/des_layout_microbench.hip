@@ -5,6 +5,9 @@
 //   d8x2   d8 with two chains interleaved per 8-lane group
 //   d4     4 lanes/chain, two SP boxes per lane (even + odd half), 2 DPP XOR steps (tdes4_kernel)
 //   d4x2   d4 with two chains interleaved per 4-lane group
+//   d4b    d4 with the next round's key-side address part computed a round early
+//   d2     2 lanes/chain, four SP boxes per lane, 1 DPP XOR step
+//   d1     1 lane/chain, all eight SP boxes, no DPP
 // All layouts run the same 48 rounds with the same per-round key words and must end
 // in the same (l, r) per chain.  Reports ns and loop cycles per Feistel round and the
 // fraction of the LDS floor (8 lookups per round per chain, 32 lanes per cycle).
@@ -13,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <type_traits>
 #include "../tlslite_amd/csrc/tg_aes3.h"
 
 using namespace tg;
@@ -70,7 +74,76 @@ struct Des8 {
     }
 };
 
-// 4 lanes per chain: tdes4_kernel's Des4 (tg_aes3.h)
+// 4 lanes per chain: tdes4_kernel's Des4 (tg_aes3.h).  2 and 1 lanes per chain: DesG,
+// lane j does the 8/LPC lookups of bytes [4j/LPC, 4(j+1)/LPC) of w and v.
+template <int LPC>
+struct DesG {
+    static constexpr int NB = 4 / LPC;
+    uint32_t be[NB], bo[NB], se[NB], so[NB];
+    __device__ __forceinline__ void init() {
+        const uint32_t lane = __lane_id(), j = lane & (LPC - 1);
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            const uint32_t b = j * NB + i;
+            be[i] = (lane & 31) * 4 + (7 - 2 * b) * 8192;
+            bo[i] = (lane & 31) * 4 + (6 - 2 * b) * 8192;
+            se[i] = (8 * b + 25u) & 31u;
+            so[i] = (8 * b + 29u) & 31u;
+        }
+    }
+    __device__ __forceinline__ uint32_t f(uint32_t te, uint32_t to) const {
+        uint32_t t[2 * NB];
+#pragma unroll
+        for (int i = 0; i < NB; i++) {
+            t[2 * i] = lds_read32((__builtin_amdgcn_alignbit(te, te, se[i]) & 0x1f80u) | be[i]);
+            t[2 * i + 1] = lds_read32((__builtin_amdgcn_alignbit(to, to, so[i]) & 0x1f80u) | bo[i]);
+        }
+#pragma unroll
+        for (int w = 1; w < 2 * NB; w *= 2)
+#pragma unroll
+            for (int i = 0; i + w < 2 * NB; i += 2 * w) t[i] ^= t[i + w];
+        uint32_t v = t[0];
+        if constexpr (LPC == 2) v ^= quad_dpp<0xB1>(v);
+        return v;
+    }
+};
+
+// d4b: Des4 with the next round's address split into a part known one round early,
+// A = (rotr(l ^ k, s) & M) | base, and the part from f: addr = A ^ (rotr(f, s) & M) -- one
+// v_alignbit + one v_bitop3 between f and the LDS read instead of bitop3, alignbit, and_or.
+__device__ __forceinline__ void d4b_rounds(const Des4& D, uint32_t& L, uint32_t& R, const uint32_t* ke,
+                                           const uint32_t* ko) {
+    constexpr uint32_t M = 0x1f80u;
+    uint32_t ae = (__builtin_amdgcn_alignbit(R ^ ke[0], R ^ ke[0], D.se) & M) | D.be;
+    uint32_t ao = (__builtin_amdgcn_alignbit(R ^ ko[0], R ^ ko[0], D.so) & M) | D.bo;
+#pragma unroll
+    for (int g = 0; g < 48; g++) {
+        uint32_t v = lds_read32(ae) ^ lds_read32(ao);
+        // the next round's key-side address part, off the critical path (l is known)
+        uint32_t ne = 0, no = 0;
+        const uint32_t lx = (g % 16 != 15) ? L : R;  // the word f is XORed onto for the next round's input
+        if (g + 1 < 48) {
+            const uint32_t te = lx ^ ke[g + 1], to = lx ^ ko[g + 1];
+            ne = (__builtin_amdgcn_alignbit(te, te, D.se) & M) | D.be;
+            no = (__builtin_amdgcn_alignbit(to, to, D.so) & M) | D.bo;
+        }
+        v ^= quad_dpp<0xB1>(v);
+        v ^= quad_dpp<0x4E>(v);
+        const uint32_t rn = L ^ v;
+        if (g % 16 != 15) {
+            if (g + 1 < 48) {
+                ae = __builtin_amdgcn_bitop3_b32(ne, __builtin_amdgcn_alignbit(v, v, D.se), M, 0x78);
+                ao = __builtin_amdgcn_bitop3_b32(no, __builtin_amdgcn_alignbit(v, v, D.so), M, 0x78);
+            }
+            L = R;
+            R = rn;
+        } else {
+            L = rn;
+            ae = ne;
+            ao = no;
+        }
+    }
+}
 
 template <int LAYOUT, int ILP>  // LAYOUT 8 or 4 lanes per chain
 __global__ void __launch_bounds__(1024) bench_kernel(uint32_t* __restrict__ out, uint64_t* __restrict__ cyc,
@@ -81,8 +154,9 @@ __global__ void __launch_bounds__(1024) bench_kernel(uint32_t* __restrict__ out,
     __builtin_amdgcn_s_setprio(1);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t grp = threadIdx.x / LAYOUT;
-    const uint32_t j = lane & (LAYOUT - 1);
+    constexpr int LPC = LAYOUT == 5 ? 4 : LAYOUT;
+    const uint32_t grp = threadIdx.x / LPC;
+    const uint32_t j = lane & (LPC - 1);
     uint32_t ch[ILP], l[ILP], r[ILP];
 #pragma unroll
     for (int i = 0; i < ILP; i++) {
@@ -90,7 +164,24 @@ __global__ void __launch_bounds__(1024) bench_kernel(uint32_t* __restrict__ out,
         l[i] = ch[i] * 2654435761u;
         r[i] = ch[i] ^ 0xdeadbeefu;
     }
-    if constexpr (LAYOUT == 8) {
+    if constexpr (LAYOUT == 5) {
+        Des4 D;
+        D.init();
+        uint32_t ke[48], ko[48];
+#pragma unroll
+        for (int g = 0; g < 48; g++) {
+            ke[g] = kev(ch[0], g);
+            ko[g] = rotl4(kod(ch[0], g));
+        }
+        for (int b = 0; b < blocks; b++) {
+            uint32_t L = l[0], R = r[0];
+            des_ip(L, R);
+            d4b_rounds(D, L, R, ke, ko);
+            des_fp(L, R);
+            l[0] = L;
+            r[0] = R;
+        }
+    } else if constexpr (LAYOUT == 8) {
         Des8 D;
         D.init();
         uint32_t kw[ILP][48];
@@ -103,7 +194,7 @@ __global__ void __launch_bounds__(1024) bench_kernel(uint32_t* __restrict__ out,
             for (int i = 0; i < ILP; i++) D.block(l[i], r[i], kw[i]);
         }
     } else {
-        Des4 D;
+        typename std::conditional<LAYOUT == 4, Des4, DesG<LAYOUT == 4 ? 1 : LAYOUT>>::type D;
         D.init();
         uint32_t ke[ILP][48], ko[ILP][48];
 #pragma unroll
@@ -170,7 +261,7 @@ struct Res {
 
 template <int LAYOUT, int ILP>
 static Res run(const char* name, int cus, int blocks) {
-    const int threads = CPC * LAYOUT / ILP;
+    const int threads = CPC * (LAYOUT == 5 ? 4 : LAYOUT) / ILP;
     auto kern = bench_kernel<LAYOUT, ILP>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               DES_LDS_BYTES);
@@ -221,6 +312,9 @@ int main(int argc, char** argv) {
     rs.push_back(run<8, 2>("d8x2", cus, blocks));
     rs.push_back(run<4, 1>("d4", cus, blocks));
     rs.push_back(run<4, 2>("d4x2", cus, blocks));
+    rs.push_back(run<5, 1>("d4b", cus, blocks));
+    rs.push_back(run<2, 1>("d2", cus, blocks));
+    rs.push_back(run<1, 1>("d1", cus, blocks));
     int bad = 0;
     for (size_t i = 1; i < rs.size(); i++)
         if (rs[i].out != rs[0].out) {
