@@ -422,15 +422,17 @@ def main():
     achieved = alg_bytes / (avg_ms / 1e3) / 1e9
     # HBM bytes per launch of the same kernel from the committed PMC summary
     # (tools/pmc_kernels.sh -> profiles/pmc_<cfg>.json), only when it names this kernel
-    traffic = None
+    traffic = seal_call_bytes = None
     tpath = args.traffic or os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
     if os.path.exists(tpath):
         try:
             pj = json.load(open(tpath))
             if pj.get("dominant_kernel") == wl.dominant_kernel():
                 traffic = pj.get("hbm_bytes_per_launch")
+                seal_call_bytes = pj.get("seal_call_hbm_bytes")
         except Exception:
-            traffic = None
+            traffic = seal_call_bytes = None
+    state_bytes = wl.cipher_state_bytes()
     lookups = wl.aes_lookups() if wl.dominant_kernel().startswith("cbc_kernel") else None
     lds = None
     if lookups:
@@ -485,7 +487,17 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": wl.dominant_kernel(), "kernel_avg_ms": round(avg_ms, 4),
-                         "alg_bytes_per_launch": alg_bytes, "lds": lds},
+                         "alg_bytes_per_launch": alg_bytes,
+                         "traffic_ratio": round(traffic / alg_bytes, 3) if traffic else None,
+                         "state_bytes_per_launch": state_bytes,
+                         "traffic_ratio_with_state": round(traffic / (alg_bytes + state_bytes), 3) if traffic else None,
+                         "seal_call_hbm_bytes": seal_call_bytes,
+                         "seal_call_ratio": round(seal_call_bytes / alg_bytes, 3) if seal_call_bytes else None,
+                         "traffic_note": "traffic / seal_call_hbm_bytes: PMC (2 FETCH_SIZE + WRITE_SIZE) of the "
+                                         "dominant kernel / of all kernels of one seal call "
+                                         "(profiles/pmc_<cfg>.json); ratios against alg_bytes (P read + 5+C "
+                                         "written) and against alg_bytes + the cipher's per-connection state",
+                         "lds": lds},
             "ms_per_seal_call": round(call_ms, 4),
             "cpu_baseline": cpu,
             "bit_exact": bit_exact,

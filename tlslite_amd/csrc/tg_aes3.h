@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_MAC_LOADONLY  cooperative MAC: loads + transposes, no compression (timing only)
 //   TG_AB_MAC_NOLOAD    cooperative MAC: compressions on register data, no loads (timing only)
 //   TG_AB_MAC_PF        chunks the cooperative MAC loop prefetches (default 2)
+//   TG_AB_MAC_LB        mac_kernel's launch bound in 256-thread blocks per CU (default 3)
 #ifndef TG_AB_MAC_PRIO
 #define TG_AB_MAC_PRIO 0
 #endif
@@ -244,9 +245,12 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
 
 // Register budget: a MAC wave must fit beside four cbc_kernel waves on a SIMD
 // (4 x 80 + 168 <= 512 VGPRs) for the pipeline to overlap the two phases: the launch
-// bound's 3 waves per SIMD caps it at 168.
+// bound's 3 waves per SIMD caps it at 168.  (TG_AB_MAC_LB: the A/B of that bound.)
+#ifndef TG_AB_MAC_LB
+#define TG_AB_MAC_LB 3
+#endif
 template <int MAC, bool SSL3, int BS = 16>
-__global__ void __launch_bounds__(256, 3) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
+__global__ void __launch_bounds__(256, TG_AB_MAC_LB) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
                                                  const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
                                                  const ConnState* __restrict__ states, int32_t* __restrict__ wire_len,
                                                  const RecMeta* __restrict__ meta, uint8_t* __restrict__ tails,

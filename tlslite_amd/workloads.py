@@ -280,6 +280,18 @@ class Workload:
         return int(16 * nr[self.launches[0][0] & 0xff] * int(blocks.sum())) if len(
             {var & 0xff for var, _, _ in self.launches}) == 1 else None
 
+    def cipher_state_bytes(self):
+        """Connection-state bytes the cipher phase must move per launch: per chain the round
+        keys it encrypts with (AES: 16 (NR+1); 3DES: 3 x 128), the CBC residue read and
+        written and the fixedIVBlock (16 + 16 + 16) -- each connection has its own keys, so
+        these are algorithmic for workloads of many one-record connections (cfg3).  0 for
+        RC4-only batches."""
+        per = {N.CIPHER_AES128: 176 + 48, N.CIPHER_AES256: 240 + 48, N.CIPHER_3DES: 384 + 24}
+        tot = 0
+        for var, _, _ in self.launches:
+            tot += per.get(var & 0xff, 0)
+        return int(tot * self.n_chains // max(1, len(self.launches)))
+
     def free(self):
         for name in ("d_pt", "d_wire", "d_len", "d_recs", "d_states", "d_states0", "d_orecs", "d_opt", "d_ostatus",
                      "d_ostates", "d_ows"):
