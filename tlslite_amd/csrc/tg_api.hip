@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <vector>
 #include <stdint.h>
 #include "tg_common.h"
@@ -448,6 +449,28 @@ bool host_pinned(const void* ptr) {
     }
     return a.type == hipMemoryTypeHost;
 }
+// Staging copies between pageable host memory and the pinned buffers: one thread moves
+// ~10 GB/s, below the link's 57 GB/s per direction, so large copies are split over a few
+// threads (at most 8: the job's share of host cores on the GPU box is 16).
+void stage_copy(void* dst, const void* src, size_t n) {
+    const size_t piece = (size_t)4 << 20;
+    unsigned hc = std::thread::hardware_concurrency();
+    unsigned T = (unsigned)((n + piece - 1) / piece);
+    T = T > 8 ? 8 : T;
+    T = hc && T > hc ? hc : T;
+    if (T <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t per = (n / T + 63) & ~(size_t)63;
+    std::vector<std::thread> th;
+    for (unsigned i = 1; i < T; i++) {
+        const size_t a = i * per, e = a + per < n ? a + per : n;
+        if (a < e) th.emplace_back([=] { memcpy((char*)dst + a, (const char*)src + a, e - a); });
+    }
+    memcpy(dst, src, per < n ? per : n);
+    for (auto& t : th) t.join();
+}
 struct SubBatch {
     uint32_t c0, c1;  // chains [c0, c1)
     size_t p0, p1;    // plaintext bytes copied H2D
@@ -620,7 +643,7 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
     auto drain = [&](size_t j) -> int {
         const int t = (int)(j % D);
         TG_HIP(hipEventSynchronize(p->out_done[t]));
-        if (!wire_direct) memcpy(wire_host + sub[j].w0, p->wire_stage[t].u8(), sub[j].w1 - sub[j].w0);
+        if (!wire_direct) stage_copy(wire_host + sub[j].w0, p->wire_stage[t].u8(), sub[j].w1 - sub[j].w0);
         return 0;
     };
     // Pinned arenas: everything is enqueued at once and ordered on the GPU (slot t's seal
@@ -634,7 +657,7 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
         const uint8_t* src = pt_host + b.p0;
         if (!pt_direct) {
             if (i >= (size_t)D) TG_HIP(hipEventSynchronize(p->in_done[t]));
-            memcpy(p->pt_stage[t].u8(), src, b.p1 - b.p0);
+            stage_copy(p->pt_stage[t].u8(), src, b.p1 - b.p0);
             src = p->pt_stage[t].u8();
         }
         if (b.p1 > b.p0) TG_HIP(hipMemcpyAsync(p->pt.u8() + b.p0, src, b.p1 - b.p0, hipMemcpyHostToDevice, p->h2d));
