@@ -95,6 +95,8 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_MAC_NOLOAD    cooperative MAC: compressions on register data, no loads (timing only)
 //   TG_AB_MAC_PF        chunks the cooperative MAC loop prefetches (default 2)
 //   TG_AB_MAC_LB        mac_kernel's launch bound in 256-thread blocks per CU (default 3)
+//   TG_AB_OLD_ADDR      byte-1 T-table address by v_perm (as the other bytes) instead of v_bitop3
+//   TG_AB_OLD_SEL       cooperative-load transposes select with v_cndmask instead of v_bitop3
 #ifndef TG_AB_MAC_PRIO
 #define TG_AB_MAC_PRIO 0
 #endif
@@ -153,13 +155,13 @@ __device__ __forceinline__ uint32_t quad_lane(uint32_t v) {
 // q ^ 2 for 0x4E): of the register pair (a, b) the lane keeps the element whose index
 // bit equals its own bit `hi` and trades the other with the partner -- it sends exactly
 // the element it overwrites.  3 VALU per pair (the DPP rides in the selects).
+#ifdef TG_AB_OLD_SEL
 template <int CTRL>
 __device__ __forceinline__ void quad_bfly(uint32_t& a, uint32_t& b, bool hi) {
     const uint32_t r = quad_dpp<CTRL>(hi ? a : b);
     a = hi ? r : a;
     b = hi ? b : r;
 }
-// lane p holds x[L] = M[L][p]  ->  lane q holds x[s] = M[q][s]   (12 VALU)
 __device__ __forceinline__ void quad_transpose4(uint32_t x[4], uint32_t q) {
     const bool b0 = (q & 1) != 0, b1 = (q & 2) != 0;
     quad_bfly<0xB1>(x[0], x[1], b0);
@@ -167,6 +169,25 @@ __device__ __forceinline__ void quad_transpose4(uint32_t x[4], uint32_t q) {
     quad_bfly<0x4E>(x[0], x[2], b1);
     quad_bfly<0x4E>(x[1], x[3], b1);
 }
+#else
+// the selects as v_bitop3 (m ? x : y, 2 cycles with all-VGPR operands) on a per-lane
+// all-ones / all-zeros mask instead of v_cndmask on a lane mask in SGPRs (4 cycles)
+template <int CTRL>
+__device__ __forceinline__ void quad_bfly(uint32_t& a, uint32_t& b, uint32_t m) {
+    const uint32_t r = quad_dpp<CTRL>(__builtin_amdgcn_bitop3_b32(m, a, b, 0xCA));
+    const uint32_t na = __builtin_amdgcn_bitop3_b32(m, r, a, 0xCA);
+    b = __builtin_amdgcn_bitop3_b32(m, b, r, 0xCA);
+    a = na;
+}
+// lane p holds x[L] = M[L][p]  ->  lane q holds x[s] = M[q][s]   (4 DPP + 8 selects)
+__device__ __forceinline__ void quad_transpose4(uint32_t x[4], uint32_t q) {
+    const uint32_t m0 = 0u - (q & 1u), m1 = 0u - ((q >> 1) & 1u);
+    quad_bfly<0xB1>(x[0], x[1], m0);
+    quad_bfly<0xB1>(x[2], x[3], m0);
+    quad_bfly<0x4E>(x[0], x[2], m1);
+    quad_bfly<0x4E>(x[1], x[3], m1);
+}
+#endif
 
 // MAC over the 64-byte chunks of the quad's four records, loaded cooperatively: per load
 // instruction lane q fetches bytes [16q, 16q+16) of record L's chunk, so a quad reads a

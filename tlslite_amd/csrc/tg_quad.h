@@ -26,14 +26,33 @@ __device__ __forceinline__ uint32_t quad_dpp(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, true);
 }
 
+// A VGPR holding a constant: gfx950 issues v_bitop3_b32 and the plain VOP2 logic ops in 2
+// cycles per wave64 only when every operand is a VGPR (or an inline / literal constant);
+// an SGPR operand, a DPP modifier, v_perm_b32, v_alignbit_b32, v_add3_u32 or v_lshlrev_b32
+// take 4 (tools/valu_rate_microbench.hip, 4 waves per SIMD).
+__device__ __forceinline__ uint32_t vconst(uint32_t c) {
+    uint32_t v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "i"(c));
+    return v;
+}
+
 struct QuadAes {
     uint32_t lo, hi;  // lane-copy offset words (table pair select in byte 2)
+    uint32_t m8;      // 0xff00 in a VGPR (byte-1 address mask)
     __device__ __forceinline__ void init() {
         lo = (__lane_id() & 31) * 4;
         hi = lo | 0x10000u;
+        m8 = vconst(0xff00u);
     }
     template <int T, int B>  // T_t[byte B of s]
     __device__ __forceinline__ uint32_t look(uint32_t s) const {
+#ifndef TG_AB_OLD_ADDR
+        if constexpr (B == 1) {
+            // byte 1 already sits at the row-index bits: (s & 0xff00) | base, one 2-cycle
+            // v_bitop3 instead of a 4-cycle v_perm
+            return lds_read32(__builtin_amdgcn_bitop3_b32(s, m8, T >= 2 ? hi : lo, 0xEA) + (T & 1) * 128);
+        }
+#endif
         constexpr uint32_t sel = 0x0c000000u | (2u << 16) | ((4u + B) << 8) | 0u;
         return lds_read32(perm(s, T >= 2 ? hi : lo, sel) + (T & 1) * 128);
     }

@@ -20,6 +20,32 @@ __device__ __forceinline__ uint32_t op(uint32_t a, uint32_t b, uint32_t c) {
     if constexpr (KIND == 4) return a + b + c;                                      // v_add3_u32
     if constexpr (KIND == 5) return __builtin_amdgcn_alignbit(a, b, c);             // v_alignbit_b32
     if constexpr (KIND == 6) return dppx<0x141>(a) ^ b;                             // v_xor_b32 dpp row_half_mirror
+    uint32_t r;
+    // inline asm: exactly this instruction, nothing the compiler can fold
+    if constexpr (KIND == 10) asm volatile("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    if constexpr (KIND == 11) asm volatile("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    if constexpr (KIND == 12) asm volatile("v_lshlrev_b32 %0, 3, %1" : "=v"(r) : "v"(a));
+    if constexpr (KIND == 13) asm volatile("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    if constexpr (KIND == 15) asm volatile("v_lshl_or_b32 %0, %1, 8, %2" : "=v"(r) : "v"(a), "v"(b));
+    if constexpr (KIND == 16) asm volatile("v_bfe_u32 %0, %1, 8, 8" : "=v"(r) : "v"(a));
+    if constexpr (KIND == 17) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(r) : "v"(a));
+    if constexpr (KIND == 18) asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    if constexpr (KIND == 19) asm volatile("v_alignbyte_b32 %0, %1, %2, 1" : "=v"(r) : "v"(a), "v"(b));
+    if constexpr (KIND == 20) asm volatile("v_cndmask_b32 %0, %1, %2, vcc" : "=v"(r) : "v"(a), "v"(b));
+    if constexpr (KIND == 21) asm volatile("v_lshrrev_b32 %0, %1, %2" : "=v"(r) : "v"(c), "v"(a));
+    if constexpr (KIND == 22) asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    if constexpr (KIND == 23) asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    if constexpr (KIND == 24) asm volatile("v_or3_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    if constexpr (KIND == 25) asm volatile("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    if constexpr (KIND == 26) asm volatile("v_lshrrev_b32_e32 %0, 8, %1" : "=v"(r) : "v"(a));
+    if constexpr (KIND == 27) asm volatile("v_and_b32_e32 %0, 0xff00, %1" : "=v"(r) : "v"(a));
+    if constexpr (KIND == 28) asm volatile("v_xor_b32_e32 %0, s8, %1" : "=v"(r) : "v"(a) : "s8");
+    if constexpr (KIND == 29) asm volatile("v_bitop3_b32 %0, %1, s8, %2 bitop3:0xec" : "=v"(r) : "v"(a), "v"(c) : "s8");
+    if constexpr (KIND == 30) asm volatile("v_or_b32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    if constexpr (KIND == 31) asm volatile("v_lshlrev_b32_e32 %0, %1, %2" : "=v"(r) : "v"(c), "v"(a));
+    if constexpr (KIND == 32) asm volatile("v_xor_b32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(r) : "v"(a), "v"(b));
+    if constexpr (KIND == 33) asm volatile("v_and_b32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    if constexpr (KIND >= 10) return r;
     return 0;
 }
 
@@ -36,14 +62,19 @@ __global__ void __launch_bounds__(1024) rate_kernel(uint32_t* out, uint64_t* cyc
 #pragma unroll
         for (int r = 0; r < 8; r++)
 #pragma unroll
-            for (int i = 0; i < 8; i++) x[i] = op<KIND>(x[i], x[i ^ 4], KIND == 3 ? x[(i + 2) & 7] : c);
+            for (int i = 0; i < 8; i++)
+                x[i] = op<KIND>(x[i], x[i ^ 4], (KIND == 3 || KIND == 13 || KIND == 14 || (KIND >= 18 && KIND != 31)) ? x[(i + 2) & 7] : KIND == 31 ? (c & 7) : c);
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     uint32_t s = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) s ^= x[i];
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
-    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+    // every wave's start and end: the block's span is max(end) - min(start)
+    if ((threadIdx.x & 63) == 0) {
+        cyc[2 * (blockIdx.x * 16 + threadIdx.x / 64)] = t0;
+        cyc[2 * (blockIdx.x * 16 + threadIdx.x / 64) + 1] = t1;
+    }
 }
 
 template <int KIND>
@@ -52,13 +83,20 @@ static void run(const char* name, int cus, int waves_per_simd, int iters) {
     uint32_t* d_out;
     uint64_t* d_cyc;
     (void)hipMalloc(&d_out, (size_t)cus * threads * 4);
-    (void)hipMalloc(&d_cyc, cus * 8);
+    (void)hipMalloc(&d_cyc, (size_t)cus * 16 * 16);
     hipLaunchKernelGGL(rate_kernel<KIND>, dim3(cus), dim3(threads), 0, 0, d_out, d_cyc, 16, 1u);
     (void)hipDeviceSynchronize();
     hipLaunchKernelGGL(rate_kernel<KIND>, dim3(cus), dim3(threads), 0, 0, d_out, d_cyc, iters, 1u);
     (void)hipDeviceSynchronize();
-    uint64_t c = 0;
-    (void)hipMemcpy(&c, d_cyc, 8, hipMemcpyDeviceToHost);
+    const int waves = threads / 64;
+    uint64_t st[32];
+    (void)hipMemcpy(st, d_cyc, (size_t)waves * 16, hipMemcpyDeviceToHost);  // block 0
+    uint64_t lo = st[0], hi = st[1];
+    for (int w = 1; w < waves; w++) {
+        lo = st[2 * w] < lo ? st[2 * w] : lo;
+        hi = st[2 * w + 1] > hi ? st[2 * w + 1] : hi;
+    }
+    const uint64_t c = hi - lo;
     const double instrs_per_simd = (double)iters * 64 * waves_per_simd;  // 8 x 8 per iteration per wave
     printf("%-22s waves/SIMD %d: %5.2f cycles per wave-instruction per SIMD\n", name, waves_per_simd,
            (double)c / instrs_per_simd);
@@ -70,14 +108,18 @@ int main() {
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const int iters = 4096;
-    for (int w : {1, 2, 4}) {
-        run<0>("v_xor_b32", cus, w, iters);
-        run<1>("v_xor_b32 dpp quad", cus, w, iters);
-        run<6>("v_xor_b32 dpp row_half", cus, w, iters);
+    for (int w : {4}) {
+        run<26>("v_lshrrev_b32 const", cus, w, iters);
+        run<27>("v_and_b32 literal", cus, w, iters);
+        run<28>("v_xor_b32 sgpr", cus, w, iters);
+        run<29>("v_bitop3_b32 sgpr", cus, w, iters);
+        run<30>("v_or_b32", cus, w, iters);
+        run<31>("v_lshlrev_b32 vgpr", cus, w, iters);
+        run<32>("v_xor_b32 dpp (asm)", cus, w, iters);
+        run<33>("v_and_b32", cus, w, iters);
+        run<10>("v_xor_b32 (asm)", cus, w, iters);
+        run<23>("v_bitop3_b32 (asm)", cus, w, iters);
         run<2>("v_perm_b32", cus, w, iters);
-        run<3>("v_bitop3_b32", cus, w, iters);
-        run<4>("v_add3_u32", cus, w, iters);
-        run<5>("v_alignbit_b32", cus, w, iters);
     }
     return 0;
 }
