@@ -35,8 +35,11 @@ struct RecMeta {
 };
 static_assert(sizeof(RecMeta) == 32, "RecMeta");
 constexpr uint32_t TAIL_SLOT = 64;
-constexpr int C3_THREADS = 1024;  // 16 cipher waves
-constexpr int C3_CHAINS = 256;
+#ifndef TG_AB_CBC_WAVES
+#define TG_AB_CBC_WAVES 16
+#endif
+constexpr int C3_THREADS = 64 * TG_AB_CBC_WAVES;  // 16 cipher waves
+constexpr int C3_CHAINS = 16 * TG_AB_CBC_WAVES;
 
 template <int CIPHER_ID, int MAC, bool SSL3>
 __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
@@ -97,6 +100,9 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_MAC_LB        mac_kernel's launch bound in 256-thread blocks per CU (default 3)
 //   TG_AB_OLD_ADDR      byte-1 T-table address by v_perm (as the other bytes) instead of v_bitop3
 //   TG_AB_OLD_SEL       cooperative-load transposes select with v_cndmask instead of v_bitop3
+//   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
+//   TG_AB_MAC_FLAT      cooperative MAC loads as flat_load (generic pointers) instead of global_load
+//   TG_AB_DES_ANDOR     3DES SP-box address by v_and_or_b32 instead of v_bitop3
 #ifndef TG_AB_MAC_PRIO
 #define TG_AB_MAC_PRIO 0
 #endif
@@ -144,6 +150,21 @@ __device__ __forceinline__ void mac_bulk(M& mac, const uint8_t* P, uint32_t nful
 #define TG_AB_MAC_PF 2
 #endif
 constexpr int MAC_PF = TG_AB_MAC_PF;  // chunks prefetched ahead by the cooperative MAC loop
+
+// 16-byte load through a global-address-space pointer: the quad's record pointers are
+// rebuilt from DPP-exchanged integers, which the compiler would otherwise turn into
+// flat_load (address space unknown)
+__device__ __forceinline__ uint4 ldg16(const uint8_t* p) {
+#if defined(TG_AB_MAC_FLAT) || !defined(__HIP_DEVICE_COMPILE__)
+    return *(const uint4*)p;
+#else
+    typedef __attribute__((address_space(1))) const uint32_t g_u32;
+    const g_u32* g = (const g_u32*)(size_t)p;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)g;
+    return make_uint4(v.x, v.y, v.z, v.w);
+#endif
+}
 
 // value of v in lane L of the calling lane's quad
 template <int L>
@@ -219,7 +240,7 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
 #ifdef TG_AB_MAC_NOLOAD
             nxt[d][L] = make_uint4(lo + L + d, hi, q, L);
 #else
-            nxt[d][L] = *(const uint4*)(PL[L] + 64 * min((uint32_t)d, NL[L]));
+            nxt[d][L] = ldg16(PL[L] + 64 * min((uint32_t)d, NL[L]));
 #endif
         }
     for (uint32_t c = 0; c < nmax; c++) {
@@ -235,7 +256,7 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
         for (int L = 0; L < 4; L++) nxt[MAC_PF - 1][L] = make_uint4(cur[L].y + c, cur[L].z ^ c, cur[L].w, cur[L].x);
 #else
 #pragma unroll
-        for (int L = 0; L < 4; L++) nxt[MAC_PF - 1][L] = *(const uint4*)(PL[L] + 64 * min(c + MAC_PF, NL[L]));
+        for (int L = 0; L < 4; L++) nxt[MAC_PF - 1][L] = ldg16(PL[L] + 64 * min(c + MAC_PF, NL[L]));
 #endif
         // component t of lane p's piece of record L = record L's word 4p + t
         uint32_t d[16], x[4];
@@ -533,9 +554,10 @@ constexpr int D4_THREADS = 512;
 constexpr int D4_CHAINS = D4_THREADS / 4;
 
 struct Des4 {
-    uint32_t be, bo, se, so;
+    uint32_t be, bo, se, so, m;
     __device__ __forceinline__ void init() {
         const uint32_t lane = __lane_id(), j = lane & 3;
+        m = vconst(0x1f80u);
         be = (lane & 31) * 4 + (7 - 2 * j) * 8192;
         bo = (lane & 31) * 4 + (6 - 2 * j) * 8192;
         // rotate so that the lane's 6 index bits (bit 8j of w, bit 8j+4 of t_odd) land at bits 7..12
@@ -546,7 +568,13 @@ struct Des4 {
     __device__ __forceinline__ uint32_t f(uint32_t te, uint32_t to) const {
         const uint32_t ue = __builtin_amdgcn_alignbit(te, te, se);
         const uint32_t uo = __builtin_amdgcn_alignbit(to, to, so);
+#ifdef TG_AB_DES_ANDOR
         uint32_t v = lds_read32((ue & 0x1f80u) | be) ^ lds_read32((uo & 0x1f80u) | bo);
+#else
+        // (u & 0x1f80) | base as an all-VGPR v_bitop3 (2 cycles) rather than v_and_or_b32 (4)
+        uint32_t v = lds_read32(__builtin_amdgcn_bitop3_b32(ue, m, be, 0xEA)) ^
+                     lds_read32(__builtin_amdgcn_bitop3_b32(uo, m, bo, 0xEA));
+#endif
         v ^= quad_dpp<0xB1>(v);
         v ^= quad_dpp<0x4E>(v);
         return v;
