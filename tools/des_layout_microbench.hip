@@ -113,9 +113,9 @@ struct DesG {
 // v_alignbit + one v_bitop3 between f and the LDS read instead of bitop3, alignbit, and_or.
 __device__ __forceinline__ void d4b_rounds(const Des4& D, uint32_t& L, uint32_t& R, const uint32_t* ke,
                                            const uint32_t* ko) {
-    constexpr uint32_t M = 0x1f80u;
-    uint32_t ae = (__builtin_amdgcn_alignbit(R ^ ke[0], R ^ ke[0], D.se) & M) | D.be;
-    uint32_t ao = (__builtin_amdgcn_alignbit(R ^ ko[0], R ^ ko[0], D.so) & M) | D.bo;
+    const uint32_t M = D.m;  // 0x1f80 in a VGPR: the bitop3 forms stay 2-cycle
+    uint32_t ae = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(R ^ ke[0], R ^ ke[0], D.se), M, D.be, 0xEA);
+    uint32_t ao = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(R ^ ko[0], R ^ ko[0], D.so), M, D.bo, 0xEA);
 #pragma unroll
     for (int g = 0; g < 48; g++) {
         uint32_t v = lds_read32(ae) ^ lds_read32(ao);
@@ -124,8 +124,8 @@ __device__ __forceinline__ void d4b_rounds(const Des4& D, uint32_t& L, uint32_t&
         const uint32_t lx = (g % 16 != 15) ? L : R;  // the word f is XORed onto for the next round's input
         if (g + 1 < 48) {
             const uint32_t te = lx ^ ke[g + 1], to = lx ^ ko[g + 1];
-            ne = (__builtin_amdgcn_alignbit(te, te, D.se) & M) | D.be;
-            no = (__builtin_amdgcn_alignbit(to, to, D.so) & M) | D.bo;
+            ne = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(te, te, D.se), M, D.be, 0xEA);
+            no = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_alignbit(to, to, D.so), M, D.bo, 0xEA);
         }
         v ^= quad_dpp<0xB1>(v);
         v ^= quad_dpp<0x4E>(v);
