@@ -229,7 +229,8 @@ def host_inclusive_rate(wl, chunk=64 << 20, depth=3):
            "pcie_measured_gbs": link,
            "pcie_ceiling": round(wl.plaintext_total / GIB / t_min, 2),
            "method": "tlsgpu_host_pipeline_seal: per sub-batch of ~chunk_bytes plaintext H2D copy, seal, D2H copy "
-                     "of its wire range on three streams (one per engine), `depth` sub-batches in flight; wall time of "
+                     "of its wire range on four event-chained streams (H2D, MAC phase, cipher phase, D2H), `depth` "
+                     "sub-batches in flight; wall time of "
                      "the synchronous call, best of 3; pcie_ceiling = plaintext / the copies' minimum time at " + how}
     with HostSealPipeline(chunk, depth) as hp:
         for name, pt_h, wire_h in (("pinned", pin_pt.array[: wl.pt_bytes], pin_wire.array[: wl.wire_bytes]),
