@@ -434,7 +434,7 @@ def main():
         except Exception:
             traffic = seal_call_bytes = None
     state_bytes = wl.cipher_state_bytes()
-    lookups = wl.aes_lookups() if wl.dominant_kernel().startswith("cbc_kernel") else None
+    lookups = wl.aes_lookups() if wl.dominant_kernel().startswith(("cbc_kernel", "lseal_kernel")) else None
     lds = None
     if lookups:
         g = lookups / (avg_ms / 1e3) / 1e9

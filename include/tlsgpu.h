@@ -228,6 +228,12 @@ int tlsgpu_seal_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_r
                     uint32_t nrecords, const uint8_t *pt, uint8_t *wire, tlsgpu_conn_state *states,
                     int32_t *wire_len, uint32_t variant, void *workspace, size_t workspace_bytes,
                     tlsgpu_stream s);
+/* AES suites: from this many chains per call on the current device, the seal runs one
+ * lane per chain with the MAC and the CBC of each record in the same lane; below it, the
+ * MAC of every record runs in parallel and each chain's CBC on four lanes.  The layouts
+ * give identical bytes.  UINT32_MAX: this build has only the split layout (the product
+ * library; the lane layout is an A/B build). */
+int tlsgpu_seal_lane_min_chains(uint32_t *nchains);
 /* ---- seal pipeline: successive tlsgpu_pipeline_seal calls overlap the MAC
  * phase of call k+1 with the cipher phase of call k (AES suites; two
  * library-owned streams, three workspaces in rotation, so the MAC phase may run

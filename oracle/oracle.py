@@ -66,7 +66,7 @@ def _load():
                                      ctypes.POINTER(ctypes.c_int)]
     lib.ora_seal_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     lib.ora_fill_pattern.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
     return lib
 
@@ -202,7 +202,7 @@ def fill_pattern(n, seed, start=0):
 
 
 def seal_batch(protos, chain_begin, chain_count, pt, pt_off, pt_len, wire, wire_off, ctype=None, nthreads=1,
-               update=False):
+               update=False, flags=None):
     """Seal many chains in parallel threads.  protos: list of Conn (one per
     chain, copied -- the originals are advanced only with update=True).
     Returns wire_len array."""
@@ -218,9 +218,10 @@ def seal_batch(protos, chain_begin, chain_count, pt, pt_off, pt_len, wire, wire_
     wire_off = np.ascontiguousarray(wire_off, dtype=np.uint64)
     wl = np.zeros(len(pt_len), dtype=np.int64)
     ct = None if ctype is None else np.ascontiguousarray(ctype, dtype=np.uint8)
+    fl = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
     L.ora_seal_batch(arr, len(protos), chain_begin.ctypes.data, chain_count.ctypes.data, pt.ctypes.data,
                      pt_off.ctypes.data, pt_len.ctypes.data, None if ct is None else ct.ctypes.data,
-                     wire.ctypes.data, wire_off.ctypes.data, wl.ctypes.data, nthreads)
+                     None if fl is None else fl.ctypes.data, wire.ctypes.data, wire_off.ctypes.data, wl.ctypes.data, nthreads)
     if update:
         for i, c in enumerate(protos):
             ctypes.memmove(c.buf, ctypes.addressof(arr) + i * sz, sz)

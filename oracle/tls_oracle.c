@@ -648,7 +648,7 @@ typedef struct {
     ora_conn *protos;   /* one per chain */
     const uint8_t *pt;        /* plaintext arena */
     const uint64_t *pt_off; const uint32_t *pt_len; const uint64_t *wire_off;
-    const uint8_t *ctype;
+    const uint8_t *ctype; const uint8_t *flags;
     uint8_t *wire;
     long *wire_len;
     const uint32_t *chain_begin; const uint32_t *chain_count;
@@ -661,7 +661,8 @@ static void *batch_worker(void *p) {
         ora_conn c = a->protos[ch];
         for (uint32_t k = 0; k < a->chain_count[ch]; k++) {
             size_t r = a->chain_begin[ch] + k;
-            a->wire_len[r] = ora_seal(&c, a->ctype ? a->ctype[r] : 23, a->pt + a->pt_off[r], a->pt_len[r], 0,
+            a->wire_len[r] = ora_seal(&c, a->ctype ? a->ctype[r] : 23, a->pt + a->pt_off[r], a->pt_len[r],
+                                      a->flags ? a->flags[r] : 0,
                                       a->wire + a->wire_off[r], (size_t)1 << 20);
         }
         a->protos[ch] = c; /* the chain's state after its records (residue, RC4, seqnum) */
@@ -671,13 +672,13 @@ static void *batch_worker(void *p) {
 
 int ora_seal_batch(ora_conn *protos, size_t nchains, const uint32_t *chain_begin, const uint32_t *chain_count,
                    const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len, const uint8_t *ctype,
-                   uint8_t *wire, const uint64_t *wire_off, long *wire_len, int nthreads) {
+                   const uint8_t *flags, uint8_t *wire, const uint64_t *wire_off, long *wire_len, int nthreads) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
     batch_arg args[256];
     for (int t = 0; t < nthreads; t++) {
-        batch_arg a = {protos, pt, pt_off, pt_len, wire_off, ctype, wire, wire_len, chain_begin, chain_count,
+        batch_arg a = {protos, pt, pt_off, pt_len, wire_off, ctype, flags, wire, wire_len, chain_begin, chain_count,
                        nchains, nthreads, t};
         args[t] = a;
         if (nthreads > 1) pthread_create(&th[t], NULL, batch_worker, &args[t]);

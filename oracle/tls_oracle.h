@@ -43,6 +43,7 @@ void ora_conn_get_rc4(const ora_conn *c, uint8_t *S256, int *i, int *j);
 size_t ora_conn_size(void);
 int ora_seal_batch(ora_conn *protos, size_t nchains, const uint32_t *chain_begin, const uint32_t *chain_count,
                    const uint8_t *pt, const uint64_t *pt_off, const uint32_t *pt_len, const uint8_t *ctype,
+                   const uint8_t *flags,
                    uint8_t *wire, const uint64_t *wire_off, long *wire_len, int nthreads);
 void ora_fill_pattern(uint8_t *p, size_t n, uint64_t seed, uint64_t start);
 #endif

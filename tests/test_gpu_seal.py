@@ -117,12 +117,13 @@ def _mixed_workload(n, pt_len, seed, suites=("AES128-SHA", "RC4-SHA")):
     return W.Workload("mixed", groups, seed, rec_order=rng.permutation(3 * n))
 
 
-@pytest.mark.parametrize("kind", ["cfg2", "mixed", "3des", "rc4_3des"])
+@pytest.mark.parametrize("kind", ["cfg2", "mixed", "3des", "rc4_3des", "lane"])
 def test_pipeline_equals_sequential(kind):
     """tlsgpu_pipeline_seal: K successive batches (MAC phase of batch k+1
     overlapping the cipher phase of batch k) give the same wire bytes and final
     connection states as K sequential tlsgpu_seal_dev calls -- for AES, the
-    3DES split path (prefix / MAC / tdes4_kernel) and RC4 + 3DES mixes."""
+    3DES split path (prefix / MAC / tdes4_kernel), RC4 + 3DES mixes, and AES
+    batches large enough for the lane kernel (tg_lane.h)."""
     _T()
     from tlslite_amd import workloads as W
     from tlslite_amd.device import DeviceBuffer, Stream
@@ -133,8 +134,13 @@ def test_pipeline_equals_sequential(kind):
         wl = _mixed_workload(300, 2000, 12)
     elif kind == "3des":
         wl = _mixed_workload(300, 2003, 13, ("3DES-SHA", "3DES-SHA"))
-    else:
+    elif kind == "rc4_3des":
         wl = _mixed_workload(300, 1999, 14, ("3DES-SHA", "RC4-SHA"))
+    else:
+        from tlslite_amd.recordlayer import seal_lane_min_chains
+        if seal_lane_min_chains() == 0xffffffff:
+            pytest.skip("lane layout not in this build (A/B build TG_AB_LANE_SEAL, DESIGN.md §5.2)")
+        wl = W.cfg3(n=seal_lane_min_chains() + 1000, pt_len=300, seed=15)
     wl.to_device()
     K = 4
     s = Stream()
@@ -328,4 +334,57 @@ def test_host_pipeline_equals_device_path(kind, pinned):
     assert np.array_equal(wl.d_states.download(), ref_states)
     for b in bufs:
         b.free()
+    wl.free()
+
+
+@pytest.mark.parametrize("suite,version", [("AES256-SHA256", (3, 3)), ("AES128-SHA", (3, 1)), ("AES128-SHA", (3, 0)),
+                                           ("AES256-SHA", (3, 2))])
+def test_lane_path_vs_oracle(suite, version):
+    """A seal call of at least tlsgpu_seal_lane_min_chains() chains runs on the lane
+    kernel (tg_lane.h: one lane per chain, MAC and CBC of a record in the same lane;
+    an A/B build, TLSGPU_LIB=tools/ab/lane/libtlsgpu.so -- skipped on the product library).
+    One launch of that many chains plus a persistent second generation -- one-record
+    connections of 1,434 B (cfg3's record), 3-record chains of 100 B, 2-record chains of
+    5,003 B, chains of sub-block, block-sized and empty records, random content types and
+    badMAC / badPadding faults on ~3 % of the records -- equals the oracle byte for byte,
+    every wire length, and every chain's final CBC residue and seqnum
+    (tlsrecordlayer.py:538-617, python_aes.py:44)."""
+    _T()
+    from tlslite_amd import workloads as W
+    from tlslite_amd.device import synchronize
+    from tlslite_amd.recordlayer import seal_lane_min_chains
+    from tests.wl_oracle import device_states, oracle_seal
+    from oracle import oracle as O
+    rng = np.random.default_rng(zlib.crc32(repr(("lane", suite, version)).encode()))
+    _, kl, ivl, _, ml = O.SUITES[suite]
+
+    def grp(nconn, recs, n):
+        ivs = np.frombuffer(rng.bytes(ivl * nconn), dtype=np.uint8).reshape(nconn, ivl)
+        return W.Group(suite, version, [rng.bytes(kl)], ivs, [rng.bytes(ml)], [rng.bytes(ivl)],
+                       rng.integers(0, 2 ** 40, nconn, dtype=np.uint64), recs, n)
+    nmin = seal_lane_min_chains()
+    if nmin == 0xffffffff:
+        pytest.skip("lane layout not in this build (A/B build TG_AB_LANE_SEAL, DESIGN.md §5.2)")
+    small = [grp(20000, 3, 100), grp(6000, 2, 5003), grp(3000, 2, 0), grp(3000, 4, 15), grp(3000, 1, 16),
+             grp(3000, 2, 63), grp(3000, 1, 64), grp(3000, 1, 65)]
+    n_big = nmin + 9000 - sum(g.nconn for g in small)
+    groups = [grp(n_big, 1, 1434)] + small
+    nrec = sum(g.nconn * g.recs_per_conn for g in groups)
+    ctype = rng.choice([21, 22, 23], nrec, p=[0.05, 0.05, 0.9])
+    flags = np.where(rng.random(nrec) < 0.03, rng.integers(1, 4, nrec), 0)
+    wl = W.Workload("lane", groups, 72, rec_ctype=ctype, rec_flags=flags)
+    wl.to_device()
+    assert [n for _, _, n in wl.launches] == [wl.n_chains] and wl.n_chains > nmin
+    wl.launch()
+    synchronize()
+    wire_gpu = wl.d_wire.download()
+    lens_gpu = wl.d_len.download().view(np.int32)
+    states = device_states(wl)
+    wire, lens, conns = oracle_seal(wl, nthreads=16)
+    assert lens_gpu.tolist() == lens.tolist()
+    bad = np.nonzero(wire_gpu != wire)[0]
+    bad_recs = sorted(set(int(np.searchsorted(wl.wire_off.astype(np.int64), x, side="right")) - 1 for x in bad[:4096]))
+    assert not len(bad), "%d bytes differ, records %s" % (len(bad), bad_recs[:20])
+    bad = [c for c, (s, o) in enumerate(zip(states, conns)) if s.iv != o.iv or s.seqnum != o.seqnum]
+    assert not bad, "chains with a wrong final state: %s" % bad[:10]
     wl.free()

@@ -29,7 +29,7 @@ def oracle_seal(wl, nthreads=8):
     pt = wl.host_plaintext(O.fill_pattern)
     wire = np.zeros(wl.wire_bytes, dtype=np.uint8)
     lens = O.seal_batch(conns, wl.chain_first, wl.chain_count, pt, wl.pt_off, wl.pt_len, wire, wl.wire_off,
-                        nthreads=nthreads, update=True)
+                        ctype=wl.rec_ctype, flags=wl.rec_flags, nthreads=nthreads, update=True)
     return wire, lens, conns
 
 

@@ -93,6 +93,7 @@ SIGNATURES = [
     ("tlsgpu_conn_state_variant", _i, [_vp, ctypes.POINTER(_u32)]),
     ("tlsgpu_seal_wire_len", _i, [_vp, _u32, ctypes.POINTER(_u32)]),
     ("tlsgpu_seal_workspace_bytes", _sz, [_u32]),
+    ("tlsgpu_seal_lane_min_chains", _i, [ctypes.POINTER(_u32)]),
     ("tlsgpu_seal_dev", _i, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
     ("tlsgpu_pipeline_create", _i, [ctypes.POINTER(_vp), _u32]),
     ("tlsgpu_pipeline_destroy", _i, [_vp]),

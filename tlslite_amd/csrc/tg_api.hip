@@ -242,6 +242,12 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state* st, uint32_t pt_len, uint32_t*
 
 size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords) { return seal_workspace_bytes(nrecords); }
 
+int tlsgpu_seal_lane_min_chains(uint32_t* nchains) {
+    if (!nchains) return fail(TLSGPU_EINVAL, "null pointer");
+    *nchains = seal_lane_min_chains();
+    return 0;
+}
+
 // library-owned workspace: one grow-only buffer per (kind, device, stream), so calls
 // on different streams never share one and calls on one stream are ordered by it
 static int own_workspace(int kind, size_t need, hipStream_t stream, uint8_t** out) {

@@ -37,39 +37,43 @@ struct Hash<TLSGPU_MAC_SHA1> {
     TG_HD static void init(uint32_t h[8]) {
         for (int i = 0; i < 5; i++) h[i] = SHA1_IV[i];
     }
-    TG_HD static void compress(uint32_t h[8], uint32_t w[16]) {
-        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
-#pragma unroll
-        for (int t = 0; t < 80; t++) {
-            uint32_t wt;
-            if (t < 16) {
-                wt = w[t];
-            } else {
-                wt = rotl32(bx3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
-                w[t & 15] = wt;
-            }
-            uint32_t f, k;
-            if (t < 20) {
-                f = bch(b, c, d);
-                k = 0x5A827999u;
-            } else if (t < 40) {
-                f = bx3(b, c, d);
-                k = 0x6ED9EBA1u;
-            } else if (t < 60) {
-                f = bmaj(b, c, d);
-                k = 0x8F1BBCDCu;
-            } else {
-                f = bx3(b, c, d);
-                k = 0xCA62C1D6u;
-            }
-            uint32_t tmp = rotl32(a, 5) + f + e + k + wt;
-            e = d;
-            d = c;
-            c = rotl32(b, 30);
-            b = a;
-            a = tmp;
+    static constexpr int ROUNDS = 80;
+    // round t on the working variables s = {a, b, c, d, e} (fully unrolled callers: the
+    // array shifts are register renames)
+    TG_HD static void round(int t, uint32_t s[8], uint32_t w[16]) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = rotl32(bx3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+            w[t & 15] = wt;
         }
-        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+        uint32_t f, k;
+        if (t < 20) {
+            f = bch(s[1], s[2], s[3]);
+            k = 0x5A827999u;
+        } else if (t < 40) {
+            f = bx3(s[1], s[2], s[3]);
+            k = 0x6ED9EBA1u;
+        } else if (t < 60) {
+            f = bmaj(s[1], s[2], s[3]);
+            k = 0x8F1BBCDCu;
+        } else {
+            f = bx3(s[1], s[2], s[3]);
+            k = 0xCA62C1D6u;
+        }
+        const uint32_t tmp = rotl32(s[0], 5) + f + s[4] + k + wt;
+        s[4] = s[3];
+        s[3] = s[2];
+        s[2] = rotl32(s[1], 30);
+        s[1] = s[0];
+        s[0] = tmp;
+    }
+    TG_HD static void compress(uint32_t h[8], uint32_t w[16]) {
+        uint32_t s[8] = {h[0], h[1], h[2], h[3], h[4], 0, 0, 0};
+#pragma unroll
+        for (int t = 0; t < 80; t++) round(t, s, w);
+        h[0] += s[0]; h[1] += s[1]; h[2] += s[2]; h[3] += s[3]; h[4] += s[4];
     }
 };
 
@@ -92,28 +96,33 @@ struct Hash<TLSGPU_MAC_SHA256> {
     TG_HD static void init(uint32_t h[8]) {
         for (int i = 0; i < 8; i++) h[i] = SHA256_IV[i];
     }
-    TG_HD static void compress(uint32_t h[8], uint32_t w[16]) {
-        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#pragma unroll
-        for (int t = 0; t < 64; t++) {
-            uint32_t wt;
-            if (t < 16) {
-                wt = w[t];
-            } else {
-                uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-                uint32_t s0 = bx3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
-                uint32_t s1 = bx3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
-                wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
-                w[t & 15] = wt;
-            }
-            uint32_t S1 = bx3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
-            uint32_t ch = bch(e, f, g);
-            uint32_t t1 = hh + S1 + ch + Sha256K::K[t] + wt;
-            uint32_t S0 = bx3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
-            uint32_t mj = bmaj(a, b, c);
-            hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+    static constexpr int ROUNDS = 64;
+    // round t on the working variables s = {a, b, c, d, e, f, g, h}
+    TG_HD static void round(int t, uint32_t s[8], uint32_t w[16]) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
+            uint32_t s0 = bx3(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+            uint32_t s1 = bx3(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
+            wt = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
+            w[t & 15] = wt;
         }
-        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+        const uint32_t S1 = bx3(rotr32(s[4], 6), rotr32(s[4], 11), rotr32(s[4], 25));
+        const uint32_t ch = bch(s[4], s[5], s[6]);
+        const uint32_t t1 = s[7] + S1 + ch + Sha256K::K[t] + wt;
+        const uint32_t S0 = bx3(rotr32(s[0], 2), rotr32(s[0], 13), rotr32(s[0], 22));
+        const uint32_t mj = bmaj(s[0], s[1], s[2]);
+        s[7] = s[6]; s[6] = s[5]; s[5] = s[4]; s[4] = s[3] + t1;
+        s[3] = s[2]; s[2] = s[1]; s[1] = s[0]; s[0] = t1 + S0 + mj;
+    }
+    TG_HD static void compress(uint32_t h[8], uint32_t w[16]) {
+        uint32_t s[8] = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]};
+#pragma unroll
+        for (int t = 0; t < 64; t++) round(t, s, w);
+#pragma unroll
+        for (int i = 0; i < 8; i++) h[i] += s[i];
     }
 };
 

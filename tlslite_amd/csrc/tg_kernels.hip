@@ -1,5 +1,6 @@
 // tg_kernels.hip -- gfx950 kernels of libtlsgpu.so and their launchers:
 //   prefix/mac/cbc_kernel, tdes4_kernel   split AES / 3DES seal (tg_aes3.h)
+//   lseal_kernel     (A/B build TG_AB_LANE_SEAL only) AES seal with one lane per chain (tg_lane.h)
 //   rc4_seal_kernel  fused per-record MAC -> RC4 -> header, one lane per connection
 //                    chain (tlsrecordlayer.py:538-617, python_rc4.py:25-41)
 //   open_*_kernel    AES open (tg_open3.h); open_kernel: RC4 / 3DES open, lane per chain
@@ -16,6 +17,9 @@
 #include "tg_quad.h"
 #include "tg_aes3.h"
 #include "tg_open3.h"
+#ifdef TG_AB_LANE_SEAL
+#include "tg_lane.h"
+#endif
 #include "tg_derive.h"
 #include "tg_launch.h"
 
@@ -441,6 +445,42 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
     }
 }
 
+// The lane-per-chain AES seal (tg_lane.h) is an A/B build (TG_AB_LANE_SEAL): on cfg3 it
+// measured slower than the split path (2.88-2.97 vs 2.71-2.75 ms per step, DESIGN.md
+// §5.2), so the product library never selects it and reports "never" (UINT32_MAX).
+#ifdef TG_AB_LANE_SEAL
+#ifndef TG_AB_LS_MIN_PER_CU
+#define TG_AB_LS_MIN_PER_CU LS_THREADS
+#endif
+uint32_t seal_lane_min_chains() { return (uint32_t)TG_AB_LS_MIN_PER_CU * cu_count(); }
+#else
+uint32_t seal_lane_min_chains() { return 0xffffffffu; }
+#endif
+static bool use_lane_seal(uint32_t nchains) { return nchains >= seal_lane_min_chains(); }
+
+#ifdef TG_AB_LANE_SEAL
+template <int NR, int MAC, bool SSL3>
+static hipError_t launch_lane_seal(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                                   uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
+                                   int32_t* wire_len, hipStream_t s) {
+    auto kern = lseal_kernel<NR, MAC, SSL3>;
+    hipError_t e = set_lds(kern, AES_LDS_BYTES);
+    if (e != hipSuccess) return e;
+    const uint32_t ncu = cu_count();
+    uint32_t grid = (nchains + LS_THREADS - 1) / LS_THREADS;
+    grid = grid > ncu ? ncu : grid;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(LS_THREADS), AES_LDS_BYTES, s, chains, nchains, recs, nrecords, pt, wire,
+                       states, wire_len);
+    return hipGetLastError();
+}
+#else
+template <int NR, int MAC, bool SSL3>
+static hipError_t launch_lane_seal(const tlsgpu_chain*, uint32_t, const tlsgpu_record*, uint32_t, const uint8_t*,
+                                   uint8_t*, ConnState*, int32_t*, hipStream_t) {
+    return hipErrorInvalidDeviceFunction;  // unreachable: use_lane_seal() is false in this build
+}
+#endif
+
 // The (cipher, MAC, SSL3) variants of the split seal path (AES and 3DES suites)
 #define TG_SPLIT_VARIANTS(X)                             \
     X(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)   \
@@ -461,6 +501,22 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
     *known = true;
     hipError_t e = hipSuccess;
 #define TG_PH(CID, NR, MAC_ID, SSL3)                                                                            \
+    if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3) && NR != 0 && use_lane_seal(nchains)) {                     \
+        /* one kernel after all earlier work of both streams; later work of both after it */                     \
+        if (s2 != s1) {                                                                                          \
+            if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                      \
+            if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                               \
+        }                                                                                                        \
+        if (cbc_start && (e = hipEventRecord(cbc_start, s2)) != hipSuccess) return e;                           \
+        e = launch_lane_seal<NR == 0 ? 10 : NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states,  \
+                                                             wire_len, s2);                                      \
+        if (e == hipSuccess && cbc_stop) e = hipEventRecord(cbc_stop, s2);                                       \
+        if (e == hipSuccess && s2 != s1) {                                                                       \
+            if ((e = hipEventRecord(mac_done, s2)) != hipSuccess) return e;                                      \
+            e = hipStreamWaitEvent(s1, mac_done, 0);                                                             \
+        }                                                                                                        \
+        return e;                                                                                                \
+    }                                                                                                            \
     if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3)) {                                                          \
         e = launch_mac_phase<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,   \
                                                epoch, s1);                                                       \

@@ -9,6 +9,7 @@ constexpr int SEAL_BLOCK = 256;  // one lane per chain, 4 waves per workgroup
 
 size_t seal_workspace_bytes(uint32_t nrecords);
 bool seal_needs_workspace(uint32_t variant);
+uint32_t seal_lane_min_chains();
 hipError_t launch_seal(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                        uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
                        uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known);

@@ -114,6 +114,15 @@ def seal_workspace_bytes(nrecords):
     return int(N.lib.tlsgpu_seal_workspace_bytes(int(nrecords)))
 
 
+def seal_lane_min_chains():
+    """Chains per AES seal call from which the current device seals one lane per chain
+    (MAC and CBC of a record in one lane, tg_lane.h) instead of the split MAC / quad-CBC
+    path.  Same bytes either way."""
+    n = ctypes.c_uint32()
+    N.call("tlsgpu_seal_lane_min_chains", ctypes.byref(n))
+    return int(n.value)
+
+
 def seal_dev(chains, nchains, records, nrecords, pt, wire, states, wire_len, variant, workspace=None, stream=None):
     """Device-resident batch seal (all pointers are DeviceBuffer / addresses).
     workspace: DeviceBuffer of >= seal_workspace_bytes(nrecords), or None for

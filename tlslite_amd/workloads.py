@@ -49,7 +49,7 @@ class Workload:
     array belongs to chain chain_of[r]; chains of one variant are launched
     together."""
 
-    def __init__(self, name, groups, seed, rec_order=None, chain_stream_start=None):
+    def __init__(self, name, groups, seed, rec_order=None, chain_stream_start=None, rec_ctype=None, rec_flags=None):
         self.name, self.groups, self.seed = name, groups, seed
         # flat records in chain order
         states, pt_len, chain_first, chain_count, chain_group = [], [], [], [], []
@@ -63,6 +63,10 @@ class Workload:
                 r += g.recs_per_conn
         self.n_records = r
         self.n_chains = len(chain_first)
+        # per-record content type / fault flags (tlsgpu_record), in chain order
+        self.rec_ctype = (np.full(r, ContentType.application_data, dtype=np.uint8) if rec_ctype is None
+                          else np.asarray(rec_ctype, dtype=np.uint8))
+        self.rec_flags = np.zeros(r, dtype=np.uint8) if rec_flags is None else np.asarray(rec_flags, dtype=np.uint8)
         self.pt_len = np.asarray(pt_len, dtype=np.uint32)
         self.chain_first = np.asarray(chain_first, dtype=np.uint32)
         self.chain_count = np.asarray(chain_count, dtype=np.uint32)
@@ -161,7 +165,7 @@ class Workload:
         self.d_pt = DeviceBuffer(self.pt_bytes)
         self.d_wire = DeviceBuffer(self.wire_bytes)
         self.d_len = DeviceBuffer(4 * self.n_records)
-        recs = make_records(self.pt_off, self.wire_off, self.pt_len, ContentType.application_data, 0)
+        recs = make_records(self.pt_off, self.wire_off, self.pt_len, self.rec_ctype, self.rec_flags)
         self.d_recs = DeviceBuffer(ctypes.sizeof(recs))
         self.d_recs.upload(np.frombuffer(recs, dtype=np.uint8))
         st = self.host_states()
@@ -258,10 +262,15 @@ class Workload:
 
     def dominant_kernel(self):
         """Name (rocprof stem) of the kernel that dominates the first launch."""
-        var = self.launches[0][0]
+        var, _, nch = self.launches[0]
         c, m = var & 0xff, (var >> 8) & 0xff
         if c in (N.CIPHER_AES128, N.CIPHER_AES256) and m in (N.MAC_SHA1, N.MAC_SHA256):
-            return "cbc_kernel<%d>" % (10 if c == N.CIPHER_AES128 else 14)
+            from .recordlayer import seal_lane_min_chains
+            nr = 10 if c == N.CIPHER_AES128 else 14
+            # many chains: one lane per chain, MAC + CBC in one kernel (tg_lane.h)
+            if nch >= seal_lane_min_chains():
+                return "lseal_kernel<%d, %d, %s>" % (nr, m, "true" if (var >> 16) & 1 else "false")
+            return "cbc_kernel<%d>" % nr
         if c == N.CIPHER_3DES:
             # split path: bench.py's events bracket the whole 3DES seal call (prefix + MAC +
             # tdes4_kernel), which tdes4_kernel dominates
