@@ -104,9 +104,9 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_MAC_FLAT      cooperative MAC loads as flat_load (generic pointers) instead of global_load
 //   TG_AB_DES_ANDOR     3DES SP-box address by v_and_or_b32 instead of v_bitop3
 //   TG_AB_LANE_SEAL     AES seal with one lane per chain for many-chain batches (tg_lane.h), with
-//                       TG_AB_LS_WAVES / TG_AB_LS_MIN_PER_CU / TG_AB_LS_NOINTERLEAVE /
-//                       TG_AB_LS_ST_EACH / TG_AB_LS_PF2 (its wave count, dispatch threshold,
-//                       hash/AES interleave, per-block stores, 2-chunk prefetch)
+//                       TG_AB_LS_WAVES / TG_AB_LS_MIN_PER_CU (its wave count and dispatch
+//                       threshold) and TG_AB_LS_NOLOAD / _NOSTORE / _NOMEM (timing only: bulk
+//                       plaintext loads / ciphertext stores / both left out)
 #ifndef TG_AB_MAC_PRIO
 #define TG_AB_MAC_PRIO 0
 #endif

@@ -97,6 +97,13 @@ __device__ __forceinline__ void lane_mix(const uint32_t t[16], const uint32_t* k
 
 template <bool AL>
 __device__ __forceinline__ void ls_load64(const uint8_t* p, uint32_t d[16]) {
+#if defined(TG_AB_LS_NOMEM) || defined(TG_AB_LS_NOLOAD)  // timing only: bulk chunks synthesised in registers
+    if constexpr (AL) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) d[q] = (uint32_t)(uintptr_t)p ^ (0x9e3779b9u * (q + 1));
+        return;
+    }
+#endif
     if constexpr (AL) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -109,20 +116,18 @@ __device__ __forceinline__ void ls_load64(const uint8_t* p, uint32_t d[16]) {
 }
 template <bool AL>
 __device__ __forceinline__ void ls_store16(uint8_t* p, const uint32_t d[4]) {
+#if defined(TG_AB_LS_NOMEM) || defined(TG_AB_LS_NOSTORE)  // timing only: no bulk ciphertext stores
+    if constexpr (AL) return;
+#endif
     if constexpr (AL) *(uint4*)p = make_uint4(d[0], d[1], d[2], d[3]);
     else store16(p, d);
 }
 
-// One 64-byte chunk: its MAC compression and its four CBC blocks, interleaved by hand.
-// The 4 x NR AES round steps are serial (CBC) and each waits on 16 LDS reads; the hash
-// rounds are serial too but independent of the AES, so ~ROUNDS / (4 NR) of them sit
-// between every round's lookups and their use (the compiler does not move the hash
-// chain into the AES waits on its own: it scheduled them as two separate sequences).
 // round step G of a chunk (compile-time recursion: every index below is a constant, so
 // the hash state, the message window and the round keys stay in named VGPRs)
 template <int NR, bool AL, class H, int G>
 __device__ __forceinline__ void ls_step(const QuadAes& A, const uint32_t cur[16], uint32_t iv[4], const uint32_t* rk,
-                                        uint8_t* O, uint32_t x[4], uint32_t s[8], uint32_t w[16], uint32_t out[16]) {
+                                        uint32_t x[4], uint32_t s[8], uint32_t w[16], uint32_t out[16]) {
     constexpr int NG = 4 * NR, SR = H::ROUNDS, B = G / NR, R = G % NR;
     constexpr int H0 = G * SR / NG, H1 = (G + 1) * SR / NG;
     static_assert(H1 - H0 <= 2, "at most two hash rounds per AES round step");
@@ -138,60 +143,46 @@ __device__ __forceinline__ void ls_step(const QuadAes& A, const uint32_t cur[16]
     if constexpr (R == NR - 1) {
 #pragma unroll
         for (int j = 0; j < 4; j++) iv[j] = out[4 * B + j] = x[j];
-#ifdef TG_AB_LS_ST_EACH
-        ls_store16<AL>(O + 16 * B, x);
-#endif
     }
-    if constexpr (G + 1 < NG) ls_step<NR, AL, H, G + 1>(A, cur, iv, rk, O, x, s, w, out);
+    if constexpr (G + 1 < NG) ls_step<NR, AL, H, G + 1>(A, cur, iv, rk, x, s, w, out);
 }
 
 // One 64-byte chunk: its MAC compression and its four CBC blocks, interleaved by hand.
 // The 4 x NR AES round steps are serial (CBC) and each waits on 16 LDS reads; the hash
 // rounds are serial too but independent of the AES, so ROUNDS / (4 NR) of them sit
 // between every round's lookups and their use (left to itself the compiler scheduled
-// the hash and the AES as two separate sequences).
+// the hash and the AES as two separate sequences).  The ciphertext goes to out[].
 template <int NR, bool AL, class M>
 __device__ __forceinline__ void ls_chunk(const QuadAes& A, M& mac, const uint32_t cur[16], uint32_t iv[4],
-                                         const uint32_t* rk, uint8_t* O) {
+                                         const uint32_t* rk, uint32_t out[16]) {
     using H = typename M::H;
     uint32_t w[16];
     mac.block_words(cur, w);
     uint32_t s[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = mac.h[i];
-    uint32_t x[4], out[16];
-    ls_step<NR, AL, H, 0>(A, cur, iv, rk, O, x, s, w, out);
-#ifndef TG_AB_LS_ST_EACH
-    // the chunk's 64 ciphertext bytes leave together: whole 64-byte pieces reach the L2
-    // instead of 16-byte ones spread over the chunk's ~10^4 cycles
-#pragma unroll
-    for (int b = 0; b < 4; b++) ls_store16<AL>(O + 16 * b, out + 4 * b);
-#endif
+    uint32_t x[4];
+    ls_step<NR, AL, H, 0>(A, cur, iv, rk, x, s, w, out);
 #pragma unroll
     for (int i = 0; i < H::NS; i++) mac.h[i] += s[i];
 #pragma unroll
     for (int i = 0; i < 4; i++) mac.prev[i] = cur[12 + i];
 }
 
-// MAC + CBC over the nfull 64-byte chunks of P (next chunk prefetched, index clamped)
+// MAC + CBC over the nfull 64-byte chunks of P (next chunk prefetched, index clamped).
+// Ciphertext leaves in whole 64-byte-aligned sectors: with thousands of records in flight
+// per XCD the L2 evicts partly written lines, and 16-byte-aligned 64-byte chunk stores
+// straddle two sectors (cfg3: WRITE_SIZE 3x the wire bytes, the bulk stores 0.37 ms of
+// a 2.9 ms kernel).  m = the blocks of the first sector that precede O; sector k >= 1 is
+// the previous chunk's last m blocks and this chunk's first 4 - m, assembled with
+// m-selects; the first sector's own blocks and the last chunk's last m blocks are stored
+// per block.
 template <int NR, bool AL, class M>
 __device__ __forceinline__ void ls_bulk(const QuadAes& A, M& mac, uint32_t iv[4], const uint32_t* rk,
                                         const uint8_t* P, uint8_t* O, uint32_t nfull) {
     if (nfull == 0) return;
-#ifdef TG_AB_LS_PF2
-    uint32_t nxt[16], nx2[16];
-    ls_load64<AL>(P, nxt);
-    ls_load64<AL>(P + 64 * (nfull > 1 ? 1 : 0), nx2);
-    for (uint32_t c = 0; c < nfull; c++) {
-        uint32_t cur[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            cur[j] = nxt[j];
-            nxt[j] = nx2[j];
-        }
-        const uint32_t cn = c + 2 < nfull ? c + 2 : nfull - 1;
-        ls_load64<AL>(P + 64 * cn, nx2);
-#else
+    const uint32_t m = AL ? ((uint32_t)(uintptr_t)O >> 4) & 3u : 0u;
+    uint32_t prv[12] = {};  // the previous chunk's blocks 1..3
     uint32_t nxt[16];
     ls_load64<AL>(P, nxt);
     for (uint32_t c = 0; c < nfull; c++) {
@@ -200,17 +191,38 @@ __device__ __forceinline__ void ls_bulk(const QuadAes& A, M& mac, uint32_t iv[4]
         for (int j = 0; j < 16; j++) cur[j] = nxt[j];
         const uint32_t cn = c + 1 < nfull ? c + 1 : c;
         ls_load64<AL>(P + 64 * cn, nxt);
-#endif
-#ifdef TG_AB_LS_NOINTERLEAVE
+        uint32_t out[16];
+        ls_chunk<NR, AL>(A, mac, cur, iv, rk, out);
+        if constexpr (!AL) {
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-            lane_cbc<NR>(A, cur + 4 * b, iv, rk);
-            ls_store16<AL>(O + 64 * c + 16 * b, iv);
+            for (int b = 0; b < 4; b++) ls_store16<AL>(O + 64 * c + 16 * b, out + 4 * b);
+        } else if (c == 0) {
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                if ((uint32_t)b + m < 4u) ls_store16<AL>(O + 16 * b, out + 4 * b);
+        } else {
+            // sector block i = E[4 - m + i] of E = [prv blocks 1..3 at E[1..3] | out blocks at E[4..7]]
+            uint32_t sec[16];
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    auto E = [&](int k) { return k >= 4 ? out[4 * (k - 4) + q] : prv[4 * (k - 1) + q]; };
+                    const uint32_t v3 = E(1 + i), v2 = E(2 + i), v1 = E(3 + i), v0 = E(4 + i);
+                    sec[4 * i + q] = m == 0 ? v0 : m == 1 ? v1 : m == 2 ? v2 : v3;
+                }
+            uint8_t* S = O + 64 * c - 16 * m;
+#pragma unroll
+            for (int b = 0; b < 4; b++) ls_store16<AL>(S + 16 * b, sec + 4 * b);
         }
-        mac.update(cur);
-#else
-        ls_chunk<NR, AL>(A, mac, cur, iv, rk, O + 64 * c);
-#endif
+#pragma unroll
+        for (int j = 0; j < 12; j++) prv[j] = out[4 + j];
+    }
+    if constexpr (AL) {  // the last chunk's last m blocks
+        uint8_t* L = O + 64 * (nfull - 1);
+#pragma unroll
+        for (int b = 1; b < 4; b++)
+            if ((uint32_t)b + m >= 4u) ls_store16<AL>(L + 16 * b, prv + 4 * (b - 1));
     }
 }
 
