@@ -232,7 +232,7 @@ int tlsgpu_seal_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_r
  * lane per chain with the MAC and the CBC of each record in the same lane; below it, the
  * MAC of every record runs in parallel and each chain's CBC on four lanes.  The layouts
  * give identical bytes.  UINT32_MAX: this build has only the split layout (the product
- * library; the lane layout is an A/B build, see DESIGN.md §5.2). */
+ * library; the lane layout is an A/B build, see DESIGN.md §3.7). */
 int tlsgpu_seal_lane_min_chains(uint32_t *nchains);
 /* ---- seal pipeline: successive tlsgpu_pipeline_seal calls overlap the MAC
  * phase of call k+1 with the cipher phase of call k (AES suites; two

@@ -139,7 +139,7 @@ def test_pipeline_equals_sequential(kind):
     else:
         from tlslite_amd.recordlayer import seal_lane_min_chains
         if seal_lane_min_chains() == 0xffffffff:
-            pytest.skip("lane layout not in this build (A/B build TG_AB_LANE_SEAL, DESIGN.md §5.2)")
+            pytest.skip("lane layout not in this build (A/B build TG_AB_LANE_SEAL, DESIGN.md §3.7)")
         wl = W.cfg3(n=seal_lane_min_chains() + 1000, pt_len=300, seed=15)
     wl.to_device()
     K = 4
@@ -364,7 +364,7 @@ def test_lane_path_vs_oracle(suite, version):
                        rng.integers(0, 2 ** 40, nconn, dtype=np.uint64), recs, n)
     nmin = seal_lane_min_chains()
     if nmin == 0xffffffff:
-        pytest.skip("lane layout not in this build (A/B build TG_AB_LANE_SEAL, DESIGN.md §5.2)")
+        pytest.skip("lane layout not in this build (A/B build TG_AB_LANE_SEAL, DESIGN.md §3.7)")
     small = [grp(20000, 3, 100), grp(6000, 2, 5003), grp(3000, 2, 0), grp(3000, 4, 15), grp(3000, 1, 16),
              grp(3000, 2, 63), grp(3000, 1, 64), grp(3000, 1, 65)]
     n_big = nmin + 9000 - sum(g.nconn for g in small)

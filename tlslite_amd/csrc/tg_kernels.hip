@@ -446,8 +446,8 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
 }
 
 // The lane-per-chain AES seal (tg_lane.h) is an A/B build (TG_AB_LANE_SEAL): on cfg3 it
-// measured slower than the split path (2.88-2.97 vs 2.71-2.75 ms per step, DESIGN.md
-// §5.2), so the product library never selects it and reports "never" (UINT32_MAX).
+// measured slower than the split path (best 2.84 vs 2.73 ms per step),
+// so the product library never selects it and reports "never" (UINT32_MAX).
 #ifdef TG_AB_LANE_SEAL
 #ifndef TG_AB_LS_MIN_PER_CU
 #define TG_AB_LS_MIN_PER_CU LS_THREADS
