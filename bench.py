@@ -279,8 +279,9 @@ def open_rate(wl, stream, steps):
     t = float(np.median(ms))
     return {"value": round(wl.plaintext_total / GIB / (t / 1e3), 2), "unit": "GiB/s", "ms": round(t, 4),
             "roundtrip_exact": ok,
-            "method": "tlsgpu_open_dev over the sealed batch (AES: block-parallel CBC decrypt, per-chain "
-                      "padding/seqnum pass, per-record MAC verify); median of HIP-event-timed calls"}
+            "method": "tlsgpu_open_dev over the sealed batch (AES / 3DES: block-parallel CBC decrypt, per-chain "
+                      "padding/seqnum pass, per-record MAC verify; RC4: lane per connection); median of "
+                      "HIP-event-timed calls"}
 
 
 def derive_rate(stream, nconn=4096, steps=10):

@@ -279,8 +279,8 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain *chains
  * on its chain (or stop at the first negative status yourself).
  * The whole decrypted body after the explicit IV (payload | MAC | padding, ct_len - IV
  * bytes) is written at pt + pt_off: size the plaintext slots for it.
- * AES suites decrypt every block of every record in parallel and need a workspace of
- * tlsgpu_open_workspace_bytes(nrecords) bytes (NULL = library-owned). */
+ * CBC suites (AES, 3DES) decrypt every block of every record in parallel and need a
+ * workspace of tlsgpu_open_workspace_bytes(nrecords) bytes (NULL = library-owned). */
 size_t tlsgpu_open_workspace_bytes(uint32_t nrecords);
 int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_open_record *records,
                     uint32_t nrecords, const uint8_t *wire, uint8_t *pt, tlsgpu_conn_state *states,

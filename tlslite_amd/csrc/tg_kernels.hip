@@ -3,7 +3,7 @@
 //   lseal_kernel     (A/B build TG_AB_LANE_SEAL only) AES seal with one lane per chain (tg_lane.h)
 //   rc4_seal_kernel  fused per-record MAC -> RC4 -> header, one lane per connection
 //                    chain (tlsrecordlayer.py:538-617, python_rc4.py:25-41)
-//   open_*_kernel    AES open (tg_open3.h); open_kernel: RC4 / 3DES open, lane per chain
+//   open_*_kernel    AES / 3DES open, block-parallel (tg_open3.h); rc4_open_kernel: RC4 open, lane per chain
 //   cipher_kernel    raw stateful CBC / RC4 encrypt+decrypt for the cipher-object
 //                    surface (python_aes.py:20-69, python_rc4.py:25-41)
 //   derive_kernel    batched _calcPendingStates (tg_derive.h)
@@ -196,122 +196,72 @@ __global__ void __launch_bounds__(SEAL_BLOCK) cipher_kernel(const tlsgpu_span* _
 }
 
 // ---------------------------------------------------------------- record open (lane)
-// _decryptRecord (tlsrecordlayer.py:958-1044) for the RC4 and 3DES suites: decrypt
-// (CBC residue / RC4 state carried), strip the TLS>=1.1 explicit IV, check padding,
-// recompute and compare the MAC.  One lane per chain; the plaintext (followed by
-// the MAC and padding bytes) is written at pt + pt_off.  status = plaintext length
-// or an alert code.  With TLSGPU_CHAIN_STOP_ON_ALERT the chain stops at its first
-// alert: later records get TLSGPU_ALERT_SKIPPED and the state stays as the failing
-// record left it (the reference closes the connection there).  AES suites open on
-// the block-parallel path (tg_open3.h).
-template <int CIPHER>
-struct OpenCipher;
-template <>
-struct OpenCipher<TLSGPU_CIPHER_3DES> {
-    using D = TdesCbc;
-    static constexpr uint32_t BS = 8, LDS = DES_LDS_BYTES;
-};
-template <>
-struct OpenCipher<TLSGPU_CIPHER_RC4> {
-    using D = Rc4Stream;
-    static constexpr uint32_t BS = 1, LDS = RC4_LDS_BYTES;
-};
-
-template <int CIPHER, int MAC, bool SSL3>
-__global__ void __launch_bounds__(SEAL_BLOCK) open_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
-                                                         const tlsgpu_open_record* __restrict__ recs,
-                                                         const uint8_t* __restrict__ wire, uint8_t* __restrict__ pt,
-                                                         ConnState* __restrict__ states,
-                                                         int32_t* __restrict__ status) {
+// _decryptRecord (tlsrecordlayer.py:958-1044) for the RC4 suites: the keystream is serial
+// per connection (python_rc4.py:30-35), so one lane per chain decrypts (RC4 state
+// carried), recomputes and compares the MAC.  The plaintext (followed by the MAC bytes)
+// is written at pt + pt_off; status = plaintext length or an alert code.  With
+// TLSGPU_CHAIN_STOP_ON_ALERT the chain stops at its first alert: later records get
+// TLSGPU_ALERT_SKIPPED and the state stays as the failing record left it (the reference
+// closes the connection there).  The CBC suites open block-parallel (tg_open3.h).
+template <int MAC, bool SSL3>
+__global__ void __launch_bounds__(SEAL_BLOCK) rc4_open_kernel(const tlsgpu_chain* __restrict__ chains,
+                                                             uint32_t nchains,
+                                                             const tlsgpu_open_record* __restrict__ recs,
+                                                             const uint8_t* __restrict__ wire,
+                                                             uint8_t* __restrict__ pt, ConnState* __restrict__ states,
+                                                             int32_t* __restrict__ status) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    constexpr bool STREAM = CIPHER == TLSGPU_CIPHER_RC4;
-    if constexpr (!STREAM) {
-        des_lds_fill(lds);
-        __syncthreads();
-    }
     const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
     ConnState* st = states + ch.state;
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
-    if (st->cipher != (uint32_t)CIPHER || st->mac != (uint32_t)MAC || st->ssl3 != (SSL3 ? 1u : 0u) || st->raw) {
+    if (st->cipher != (uint32_t)TLSGPU_CIPHER_RC4 || st->mac != (uint32_t)MAC || st->ssl3 != (SSL3 ? 1u : 0u) ||
+        st->raw) {
         for (uint32_t k = 0; k < ch.count; k++) status[ch.first + k] = TLSGPU_EMISMATCH;
         return;
     }
     const bool stop = (ch.flags & TLSGPU_CHAIN_STOP_ON_ALERT) != 0;
-    typename OpenCipher<CIPHER>::D dc;
+    Rc4Stream dc;
     dc.load(st, lds);
     uint64_t seq = st->seqnum;
     for (uint32_t k = 0; k < ch.count; k++) {
         const tlsgpu_open_record R = recs[ch.first + k];
         const uint8_t* Cb = wire + R.ct_off;
         uint8_t* Pb = pt + R.pt_off;
-        const uint32_t L = R.ct_len;
-        uint32_t len, totalPad = 0;
-        bool padGood = true;
-        int32_t res;
-        if constexpr (!STREAM) {
-            constexpr uint32_t BS = OpenCipher<CIPHER>::BS;
-            const uint32_t E = st->explicit_iv ? BS : 0u;
-            if (L % BS) {  // :964-968
-                res = TLSGPU_ALERT_DECRYPTION_FAILED;
-                goto done;
-            }
-            for (uint32_t off = 0; off < L; off += BS) {
-                uint32_t d[2];
-                load8(Cb + off, d);
-                dc.dec_block(d);
-                if (off >= E) store8(Pb + off - E, d);
-            }
-            len = L > E ? L - E : 0u;  // :970-971 (b[E:] of a shorter b is empty)
-            if (len == 0) {            // :973-977
-                res = TLSGPU_ALERT_DECRYPTION_FAILED;
-                goto done;
-            }
-            const uint32_t pl = Pb[len - 1];
-            if (pl + 1 > len) {  // :981-983
-                padGood = false;
-            } else {
-                totalPad = pl + 1;
-                if (!SSL3) {  // TLS: every padding byte must equal the length (:986-993)
-                    for (uint32_t i = len - totalPad; i < len - 1; i++)
-                        if (Pb[i] != pl) padGood = false;
-                    if (!padGood) totalPad = 0;
-                }
-            }
+        const uint32_t len = R.ct_len;
+        bool macGood = true;
+        uint32_t n = 0;
+        if ((uint32_t)DL > len) {  // :1006-1007
+            for (uint32_t i = 0; i < len; i++) Pb[i] = (uint8_t)(Cb[i] ^ dc.R.ks());
+            macGood = false;
         } else {
-            for (uint32_t i = 0; i < L; i++) Pb[i] = (uint8_t)(Cb[i] ^ dc.R.ks());
-            len = L;
-        }
-        {
-            bool macGood = true;
-            const uint32_t endLen = DL + totalPad;
-            uint32_t n = 0;
-            if (endLen > len) {  // :1006-1007
-                macGood = false;
-            } else {
-                n = len - endLen;
-                M mac;
-                mac.begin(st, seq, R.content_type, n);
-                const uint32_t nfull = n >> 6;
-                for (uint32_t c = 0; c < nfull; c++) {
-                    uint32_t cur[16];
-                    load64(Pb + 64 * c, cur);
-                    mac.update(cur);
-                }
-                uint32_t tail[16];
-                load_partial(Pb + 64 * nfull, n & 63, tail);
-                uint32_t m[8];
-                mac.finish(tail, (int)(n & 63), n, st, m);
-                seq++;  // getSeqNumBytes (:1018) runs whenever the MAC is computed
-#pragma unroll
-                for (int i = 0; i < DL; i++)
-                    if (Pb[n + i] != (uint8_t)(m[i >> 2] >> (8 * (i & 3)))) macGood = false;
+            n = len - DL;
+            M mac;
+            mac.begin(st, seq, R.content_type, n);
+            // whole 64-byte payload chunks: decrypt and MAC from the same registers (the
+            // plaintext is not read back), then the last n & 63 payload bytes and the MAC
+            // bytes one at a time
+            const uint32_t nfull = n >> 6;
+            for (uint32_t c = 0; c < nfull; c++) {
+                uint32_t cur[16];
+                load64(Cb + 64 * c, cur);
+                dc.enc64(cur);
+                store64(Pb + 64 * c, cur);
+                mac.update(cur);
             }
-            res = (padGood && macGood) ? (int32_t)n : TLSGPU_ALERT_BAD_RECORD_MAC;
+            for (uint32_t i = 64 * nfull; i < len; i++) Pb[i] = (uint8_t)(Cb[i] ^ dc.R.ks());
+            uint32_t tail[16];
+            load_partial(Pb + 64 * nfull, n & 63, tail);
+            uint32_t m[8];
+            mac.finish(tail, (int)(n & 63), n, st, m);
+            seq++;  // getSeqNumBytes (:1018) runs whenever the MAC is computed
+#pragma unroll
+            for (int i = 0; i < DL; i++)
+                if (Pb[n + i] != (uint8_t)(m[i >> 2] >> (8 * (i & 3)))) macGood = false;
         }
-    done:
+        const int32_t res = macGood ? (int32_t)n : TLSGPU_ALERT_BAD_RECORD_MAC;
         status[ch.first + k] = res;
         if (stop && res < 0) {
             for (uint32_t j = k + 1; j < ch.count; j++) status[ch.first + j] = TLSGPU_ALERT_SKIPPED;
@@ -355,15 +305,14 @@ static uint32_t cu_count() {
     return (uint32_t)ncu[dev];
 }
 
-template <int CIPHER, int MAC, bool SSL3>
-static hipError_t launch_open_t(const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
-                                const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s) {
-    auto kern = open_kernel<CIPHER, MAC, SSL3>;
-    constexpr uint32_t lds = OpenCipher<CIPHER>::LDS;
-    hipError_t e = set_lds(kern, lds);
+template <int MAC, bool SSL3>
+static hipError_t launch_rc4_open(const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
+                                  const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s) {
+    auto kern = rc4_open_kernel<MAC, SSL3>;
+    hipError_t e = set_lds(kern, RC4_LDS_BYTES);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((n + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), lds, s, chains, n, recs, wire,
-                       pt, states, status);
+    hipLaunchKernelGGL(kern, dim3((n + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), RC4_LDS_BYTES, s, chains, n, recs,
+                       wire, pt, states, status);
     return hipGetLastError();
 }
 
@@ -623,30 +572,39 @@ hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, 
 // ---------------------------------------------------------------- open launchers
 size_t open_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * sizeof(OpenMeta); }
 
-// AES suites (every AES variant: SHA1 TLS/SSL3, SHA256 TLS 1.2) open block-parallel
+// CBC suites (every AES variant: SHA1 TLS/SSL3, SHA256 TLS 1.2; 3DES-SHA) open block-parallel
 static bool open_split_variant(uint32_t v) {
     const uint32_t c = v & 0xff;
-    return c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256;
+    return c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256 || c == TLSGPU_CIPHER_3DES;
 }
 bool open_needs_workspace(uint32_t variant) { return open_split_variant(variant); }
 
+// NR 0 = 3DES (8-byte blocks, open_tdes_kernel)
 template <int NR, int MAC, bool SSL3>
 static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* recs,
                                     uint32_t nrecords, const uint8_t* wire, uint8_t* pt, ConnState* states,
                                     int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s) {
-    constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : TLSGPU_CIPHER_AES256;
+    constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
     OpenMeta* meta = reinterpret_cast<OpenMeta*>(ws);
     hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(OpenMeta), s);
     if (e != hipSuccess) return e;
     const dim3 gc((nchains + 255) / 256), gr((nrecords + 255) / 256);
     hipLaunchKernelGGL((open_prefix_kernel<CID, MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords,
                        wire, states, status, meta, epoch);
-    auto dec = open_dec_kernel<NR>;
-    if ((e = set_lds(dec, AES_DEC_LDS_BYTES)) != hipSuccess) return e;
-    uint32_t grid = (nrecords + (O3_THREADS / 64) - 1) / (O3_THREADS / 64);
-    grid = grid > cu_count() ? cu_count() : (grid ? grid : 1u);
-    hipLaunchKernelGGL(dec, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s, recs, nrecords, wire, pt, states, meta,
-                       epoch);
+    if constexpr (NR == 0) {
+        if ((e = set_lds(open_tdes_kernel, DES_LDS_BYTES)) != hipSuccess) return e;
+        uint32_t grid = (nrecords + (OT_THREADS / 64) - 1) / (OT_THREADS / 64);
+        grid = grid > cu_count() ? cu_count() : (grid ? grid : 1u);
+        hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire, pt,
+                           states, meta, epoch);
+    } else {
+        auto dec = open_dec_kernel<NR == 0 ? 10 : NR>;
+        if ((e = set_lds(dec, AES_DEC_LDS_BYTES)) != hipSuccess) return e;
+        uint32_t grid = (nrecords + (O3_THREADS / 64) - 1) / (O3_THREADS / 64);
+        grid = grid > cu_count() ? cu_count() : (grid ? grid : 1u);
+        hipLaunchKernelGGL(dec, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s, recs, nrecords, wire, pt, states,
+                           meta, epoch);
+    }
     hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords, pt, states,
                        status, meta, epoch);
     hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status, meta,
@@ -670,17 +628,17 @@ hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nc
     TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false)
     TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)
     TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)
+    TG_OPEN3(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, false)
+    TG_OPEN3(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, true)
 #undef TG_OPEN3
-#define TG_OPEN_CASE(CIPHER_ID, MAC_ID, SSL3)                 \
-    if (variant == TLSGPU_VARIANT(CIPHER_ID, MAC_ID, SSL3)) \
-        return launch_open_t<CIPHER_ID, MAC_ID, SSL3>(chains, nchains, recs, wire, pt, states, status, s);
-    TG_OPEN_CASE(TLSGPU_CIPHER_3DES, TLSGPU_MAC_SHA1, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_SHA1, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_MD5, false)
-    TG_OPEN_CASE(TLSGPU_CIPHER_3DES, TLSGPU_MAC_SHA1, true)
-    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_SHA1, true)
-    TG_OPEN_CASE(TLSGPU_CIPHER_RC4, TLSGPU_MAC_MD5, true)
-#undef TG_OPEN_CASE
+#define TG_OPEN_RC4(MAC_ID, SSL3)                                      \
+    if (variant == TLSGPU_VARIANT(TLSGPU_CIPHER_RC4, MAC_ID, SSL3)) \
+        return launch_rc4_open<MAC_ID, SSL3>(chains, nchains, recs, wire, pt, states, status, s);
+    TG_OPEN_RC4(TLSGPU_MAC_SHA1, false)
+    TG_OPEN_RC4(TLSGPU_MAC_MD5, false)
+    TG_OPEN_RC4(TLSGPU_MAC_SHA1, true)
+    TG_OPEN_RC4(TLSGPU_MAC_MD5, true)
+#undef TG_OPEN_RC4
     *known = false;
     return hipSuccess;
 }

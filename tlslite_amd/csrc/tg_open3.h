@@ -1,4 +1,4 @@
-// tg_open3.h -- block-parallel AES record open (the AES open path).
+// tg_open3.h -- block-parallel record open for the CBC suites (AES and 3DES).
 //
 // _decryptRecord (tlsrecordlayer.py:958-1044) per record is: CBC-decrypt the
 // body, drop the explicit IV, check the padding, compute the MAC with the next
@@ -13,6 +13,8 @@
 //                       lane, DPP quad exchange), two blocks per quad; waves
 //                       walk records, 32 blocks of one record per step --
 //                       every block of every record in parallel.
+//   open_tdes_kernel    the 3DES suites' decrypt: one lane per 8-byte block,
+//                       64 blocks of one record per wave step.
 //   open_seq_kernel     one lane per chain: padding check (:979-993) on the
 //                       decrypted tail, which decides whether the MAC is
 //                       computed and so whether a seqnum is consumed (:1018).
@@ -110,8 +112,9 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
     ConnState* st = states + ch.state;
     const bool ok = st->cipher == (uint32_t)CIPHER_ID && st->mac == (uint32_t)MAC &&
                     st->ssl3 == (SSL3 ? 1u : 0u) && !st->raw;
-    const uint32_t E = st->explicit_iv ? 16u : 0u;
-    uint32_t res[4] = {st->iv[0], st->iv[1], st->iv[2], st->iv[3]};
+    constexpr uint32_t BS = CIPHER_ID == TLSGPU_CIPHER_3DES ? 8u : 16u;
+    const uint32_t E = st->explicit_iv ? BS : 0u;
+    uint32_t res[4] = {st->iv[0], st->iv[1], BS == 16 ? st->iv[2] : 0u, BS == 16 ? st->iv[3] : 0u};
     for (uint32_t k = 0; k < ch.count; k++) {
         const uint32_t r = ch.first + k;
         if (r >= nrecords) break;
@@ -130,10 +133,13 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
         } else {
             const tlsgpu_open_record R = recs[r];
             const uint32_t L = R.ct_len;
-            if (L & 15u) {  // :964-968 -- not decrypted, residue unchanged
+            if (L & (BS - 1)) {  // :964-968 -- not decrypted, residue unchanged
                 status[r] = TLSGPU_ALERT_DECRYPTION_FAILED;
             } else {
-                if (L) load16(wire + R.ct_off + L - 16, res);  // decrypt() keeps the last block
+                if (L) {  // decrypt() keeps the last block
+                    if constexpr (BS == 16) load16(wire + R.ct_off + L - 16, res);
+                    else load8(wire + R.ct_off + L - 8, res);
+                }
                 if (L <= E) {                                  // :970-977 nothing left after the IV
                     status[r] = TLSGPU_ALERT_DECRYPTION_FAILED;
                 } else {
@@ -146,7 +152,7 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
     }
     if (ok) {
 #pragma unroll
-        for (int i = 0; i < 4; i++) st->iv[i] = res[i];
+        for (int i = 0; i < (int)BS / 4; i++) st->iv[i] = res[i];
     }
 }
 
@@ -185,6 +191,102 @@ open_dec_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
             aes.decrypt2<NR>(ca, cb, k);
             if (va && 16 * ba >= E) st32(P + 16 * ba - E, ca ^ pa, al);
             if (vb && 16 * bb >= E) st32(P + 16 * bb - E, cb ^ pb, al);
+        }
+    }
+}
+
+// 3DES suites (openssl_tripledes.py:40-47: P_i = D(C_i) ^ C_{i-1}): every 8-byte block of
+// every record decrypted in parallel, one lane per block (all eight SP lookups of a round in
+// the lane, no cross-lane step: the block count, not a round's latency, is what there is
+// to exploit here).  A wave walks a record 64 blocks at a time; the record -- and so the
+// connection's 96 subkey words -- is uniform over the wave, so the subkeys are scalar
+// loads.  LDS: the 64 KiB SP tables, 32 lane copies (conflict-free).
+constexpr int OT_THREADS = 1024;
+
+// DES on one lane, rotated halves as des_rounds() (tg_device.h), SP tables at LDS byte
+// (K * 64 + x) * 128 + copy * 4 (des_lds_fill).  w = r ^ k_even and t = r ^ rotl4(k_odd):
+// box 7-2j takes bits [8j, 8j+6) of w, box 6-2j bits [8j+4, 8j+10) of t, each moved to
+// bits 7..12 by one shift (one rotate for the window that wraps) and masked with the
+// lane-copy offset OR-ed in by one all-VGPR v_bitop3; the table offset rides in the
+// ds_read offset field.
+struct DesLane {
+    uint32_t lo, m;
+    __device__ __forceinline__ void init() {
+        lo = (__lane_id() & 31) * 4;
+        m = vconst(0x1f80u);
+    }
+    __device__ __forceinline__ uint32_t sp(uint32_t u, uint32_t k) const {
+        return lds_read32(__builtin_amdgcn_bitop3_b32(u, m, lo, 0xEA) + k * 8192u);
+    }
+    __device__ __forceinline__ uint32_t f(uint32_t w, uint32_t t) const {
+        const uint32_t x1 = bx3(sp(w << 7, 7), sp(w >> 1, 5), sp(w >> 9, 3));
+        const uint32_t x2 = bx3(sp(w >> 17, 1), sp(t << 3, 6), sp(t >> 5, 4));
+        const uint32_t x3 = sp(t >> 13, 2) ^ sp(__builtin_amdgcn_alignbit(t, t, 21), 0);
+        return bx3(x1, x2, x3);
+    }
+    // 16 rounds with subkey words ks[2k] (even) / ks[2k+1] (odd), k walked backwards when DEC;
+    // leaves (l, r) = (R16, L16) like des_rounds
+    template <bool DEC>
+    __device__ __forceinline__ void rounds(uint32_t& l, uint32_t& r, const uint32_t* ks) const {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int k = DEC ? 15 - i : i;
+            const uint32_t ko = ks[2 * k + 1];
+            const uint32_t t = l ^ f(r ^ ks[2 * k], r ^ ((ko << 4) | (ko >> 28)));
+            l = r;
+            r = t;
+        }
+        const uint32_t t = l;
+        l = r;
+        r = t;
+    }
+    // 3DES-EDE decrypt of one block given as two big-endian words (tdes_block<true>)
+    __device__ __forceinline__ void decrypt(uint32_t& hi, uint32_t& lo_w, const uint32_t* ks) const {
+        uint32_t l = hi, r = lo_w;
+        des_ip(l, r);
+        rounds<true>(l, r, ks + 64);
+        rounds<false>(l, r, ks + 32);
+        rounds<true>(l, r, ks);
+        des_fp(l, r);
+        hi = l;
+        lo_w = r;
+    }
+};
+__global__ void __launch_bounds__(OT_THREADS, 1)
+open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
+                 uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
+                 uint32_t epoch) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t ot_lds[];
+    des_lds_fill(ot_lds);  // the kernel's only LDS: the tables start at LDS byte 0
+    __syncthreads();
+    DesLane L;
+    L.init();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (OT_THREADS / 64);
+    for (uint32_t r = blockIdx.x * (OT_THREADS / 64) + wv; r < nrecords; r += nwaves) {
+        const OpenMeta& mt = meta[r];
+        if (mt.epoch != epoch || !(mt.flags & OM_DEC)) continue;
+        const ConnState* st = states + mt.state;
+        const uint32_t* ks = &st->des[0][0];
+        const tlsgpu_open_record R = recs[r];
+        const uint32_t E = st->explicit_iv ? 8u : 0u;
+        const uint32_t nb = R.ct_len >> 3;
+        const uint8_t* C = wire + R.ct_off;
+        uint8_t* P = pt + R.pt_off;
+        for (uint32_t b = lane; b < nb; b += 64) {
+            uint32_t c[2], p[2];
+            load8(C + 8 * b, c);
+            if (b == 0) {
+                p[0] = mt.pred[0];
+                p[1] = mt.pred[1];
+            } else {
+                load8(C + 8 * (b - 1), p);
+            }
+            uint32_t hi = bswap32(c[0]), lo = bswap32(c[1]);
+            L.decrypt(hi, lo, ks);
+            uint32_t d[2] = {bswap32(hi) ^ p[0], bswap32(lo) ^ p[1]};
+            if (8 * b >= E) store8(P + 8 * b - E, d);
         }
     }
 }
@@ -293,9 +395,15 @@ __global__ void __launch_bounds__(256) open_stop_kernel(const tlsgpu_chain* __re
         st->seqnum = m.seq + ((m.flags & OM_VERIFY) ? 1u : 0u);
         const tlsgpu_open_record R = recs[r];
         uint32_t res[4] = {m.pred[0], m.pred[1], m.pred[2], m.pred[3]};
-        if (R.ct_len && !(R.ct_len & 15u)) load16(wire + R.ct_off + R.ct_len - 16, res);
+        if (st->cipher == (uint32_t)TLSGPU_CIPHER_3DES) {
+            if (R.ct_len && !(R.ct_len & 7u)) load8(wire + R.ct_off + R.ct_len - 8, res);
+            st->iv[0] = res[0];
+            st->iv[1] = res[1];
+        } else {
+            if (R.ct_len && !(R.ct_len & 15u)) load16(wire + R.ct_off + R.ct_len - 16, res);
 #pragma unroll
-        for (int i = 0; i < 4; i++) st->iv[i] = res[i];
+            for (int i = 0; i < 4; i++) st->iv[i] = res[i];
+        }
         return;
     }
 }
