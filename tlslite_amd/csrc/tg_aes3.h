@@ -103,6 +103,8 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
 //   TG_AB_MAC_FLAT      cooperative MAC loads as flat_load (generic pointers) instead of global_load
 //   TG_AB_DES_ANDOR     3DES SP-box address by v_and_or_b32 instead of v_bitop3
+//   TG_AB_OPEN_QUAD     AES open decrypt on the quad layout (open_dec_kernel, round 1) instead of
+//                       one lane per block (open_aes_kernel)
 //   TG_AB_LANE_SEAL     AES seal with one lane per chain for many-chain batches (tg_lane.h), with
 //                       TG_AB_LS_WAVES / TG_AB_LS_MIN_PER_CU (its wave count and dispatch
 //                       threshold) and TG_AB_LS_NOLOAD / _NOSTORE / _NOMEM (timing only: bulk

@@ -598,7 +598,11 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
         hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire, pt,
                            states, meta, epoch);
     } else {
+#ifdef TG_AB_OPEN_QUAD
         auto dec = open_dec_kernel<NR == 0 ? 10 : NR>;
+#else
+        auto dec = open_aes_kernel<NR == 0 ? 10 : NR>;
+#endif
         if ((e = set_lds(dec, AES_DEC_LDS_BYTES)) != hipSuccess) return e;
         uint32_t grid = (nrecords + (O3_THREADS / 64) - 1) / (O3_THREADS / 64);
         grid = grid > cu_count() ? cu_count() : (grid ? grid : 1u);

@@ -13,8 +13,9 @@
 //                       lane, DPP quad exchange), two blocks per quad; waves
 //                       walk records, 32 blocks of one record per step --
 //                       every block of every record in parallel.
-//   open_tdes_kernel    the 3DES suites' decrypt: one lane per 8-byte block,
-//                       64 blocks of one record per wave step.
+//   open_aes_kernel /   the decrypt with one lane per block (16 / 8 bytes), 64
+//   open_tdes_kernel    blocks of one record per wave step (round 2; the quad
+//                       open_dec_kernel is the A/B build TG_AB_OPEN_QUAD).
 //   open_seq_kernel     one lane per chain: padding check (:979-993) on the
 //                       decrypted tail, which decides whether the MAC is
 //                       computed and so whether a seqnum is consumed (:1018).
@@ -191,6 +192,70 @@ open_dec_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
             aes.decrypt2<NR>(ca, cb, k);
             if (va && 16 * ba >= E) st32(P + 16 * ba - E, ca ^ pa, al);
             if (vb && 16 * bb >= E) st32(P + 16 * bb - E, cb ^ pb, al);
+        }
+    }
+}
+
+// AES decrypt with one lane per block (equivalent inverse cipher, aes_decrypt's column
+// order, FIPS-197 5.3.5): the lane does all 16 Td lookups of a round, so the quad's DPP
+// XOR tree is gone (the decrypt is throughput-bound: every block of every record is
+// independent), and a wave's 64 lanes read and write 1 KiB of contiguous ciphertext /
+// plaintext per instruction.  A wave walks one record 64 blocks at a time: the record's
+// round keys are wave-uniform scalar loads.
+template <int NR>
+__device__ __forceinline__ void lane_aes_dec(const QuadAesDec& D, uint32_t s[4], const uint32_t* dk) {
+    const QuadAes& A = D.t;
+    uint32_t s0 = s[0] ^ dk[0], s1 = s[1] ^ dk[1], s2 = s[2] ^ dk[2], s3 = s[3] ^ dk[3];
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        const uint32_t* k = dk + 4 * r;
+        const uint32_t t0 = bx3(bx3(A.look<0, 0>(s0), A.look<1, 1>(s3), A.look<2, 2>(s2)), A.look<3, 3>(s1), k[0]);
+        const uint32_t t1 = bx3(bx3(A.look<0, 0>(s1), A.look<1, 1>(s0), A.look<2, 2>(s3)), A.look<3, 3>(s2), k[1]);
+        const uint32_t t2 = bx3(bx3(A.look<0, 0>(s2), A.look<1, 1>(s1), A.look<2, 2>(s0)), A.look<3, 3>(s3), k[2]);
+        const uint32_t t3 = bx3(bx3(A.look<0, 0>(s3), A.look<1, 1>(s2), A.look<2, 2>(s1)), A.look<3, 3>(s0), k[3]);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+    }
+    const uint32_t* k = dk + 4 * NR;
+    s[0] = (D.isb<0>(s0) | D.isb<1>(s3) | D.isb<2>(s2) | D.isb<3>(s1)) ^ k[0];
+    s[1] = (D.isb<0>(s1) | D.isb<1>(s0) | D.isb<2>(s3) | D.isb<3>(s2)) ^ k[1];
+    s[2] = (D.isb<0>(s2) | D.isb<1>(s1) | D.isb<2>(s0) | D.isb<3>(s3)) ^ k[2];
+    s[3] = (D.isb<0>(s3) | D.isb<1>(s2) | D.isb<2>(s1) | D.isb<3>(s0)) ^ k[3];
+}
+
+template <int NR>
+__global__ void __launch_bounds__(O3_THREADS, 1)
+open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
+                uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
+                uint32_t epoch) {
+    aes_lds_fill(nullptr, true);
+    __syncthreads();
+    QuadAesDec D;
+    D.init();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t nwaves = gridDim.x * (O3_THREADS / 64);
+    for (uint32_t r = blockIdx.x * (O3_THREADS / 64) + wv; r < nrecords; r += nwaves) {
+        const OpenMeta& mt = meta[r];
+        if (mt.epoch != epoch || !(mt.flags & OM_DEC)) continue;
+        const ConnState* st = states + mt.state;
+        const tlsgpu_open_record R = recs[r];
+        const uint32_t E = st->explicit_iv ? 16u : 0u;
+        const uint32_t nb = R.ct_len >> 4;
+        const uint8_t* C = wire + R.ct_off;
+        uint8_t* P = pt + R.pt_off;
+        for (uint32_t b = lane; b < nb; b += 64) {
+            uint32_t c[4], p[4];
+            load16(C + 16 * b, c);
+            if (b == 0) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) p[i] = mt.pred[i];
+            } else {
+                load16(C + 16 * (b - 1), p);
+            }
+            lane_aes_dec<NR>(D, c, st->dk);
+#pragma unroll
+            for (int i = 0; i < 4; i++) c[i] ^= p[i];
+            if (16 * b >= E) store16(P + 16 * b - E, c);
         }
     }
 }
