@@ -239,7 +239,8 @@ class Workload:
         self.d_opt = DeviceBuffer(self.wire_bytes)
         self.d_ostatus = DeviceBuffer(4 * self.n_records)
         self.d_ostates = DeviceBuffer(self.d_states0.nbytes)
-        self.d_ows = DeviceBuffer(max(open_workspace_bytes(self.n_records), 16))
+        # one open workspace per launch: variants may run concurrently on separate streams
+        self.d_ows = [DeviceBuffer(max(open_workspace_bytes(self.n_records), 16)) for _ in self.launches]
         return self
 
     def opened_plaintext_matches(self):
@@ -251,14 +252,16 @@ class Workload:
                 return False
         return True
 
-    def open_launch(self, stream=None, reset=True):
-        """Open every record of the wire arena once (one call per variant)."""
+    def open_launch(self, stream=None, reset=True, streams=None):
+        """Open every record of the wire arena once (one call per variant; with several
+        streams the variants run concurrently -- they touch disjoint records and states)."""
         if reset:
             N.call("tlsgpu_memcpy_d2d", self.d_ostates.ptr, self.d_states0.ptr, self.d_ostates.nbytes,
                    stream.handle if stream else None)
-        for var, d_ch, nch in self.launches:
+        for i, (var, d_ch, nch) in enumerate(self.launches):
+            s = streams[i % len(streams)] if streams else stream
             open_dev(d_ch, nch, self.d_orecs, self.n_records, self.d_wire, self.d_opt, self.d_ostates,
-                     self.d_ostatus, var, self.d_ows, stream)
+                     self.d_ostatus, var, self.d_ows[i], s)
 
     def dominant_kernel(self):
         """Name (rocprof stem) of the kernel that dominates the first launch."""
@@ -303,11 +306,11 @@ class Workload:
 
     def free(self):
         for name in ("d_pt", "d_wire", "d_len", "d_recs", "d_states", "d_states0", "d_orecs", "d_opt", "d_ostatus",
-                     "d_ostates", "d_ows"):
+                     "d_ostates"):
             b = getattr(self, name, None)
             if b is not None:
                 b.free()
-        for b in getattr(self, "d_ws", []):
+        for b in getattr(self, "d_ws", []) + getattr(self, "d_ows", []):
             b.free()
         for _, d, _ in getattr(self, "launches", []):
             d.free()
