@@ -99,6 +99,7 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_MAC_PF        chunks the cooperative MAC loop prefetches (default 2)
 //   TG_AB_MAC_LB        mac_kernel's launch bound in 256-thread blocks per CU (default 3)
 //   TG_AB_OLD_ADDR      byte-1 T-table address by v_perm (as the other bytes) instead of v_bitop3
+//   TG_AB_FINAL_DPP     AES quad round's last XOR as v_xor_b32_dpp on z (s_nop on the critical path)
 //   TG_AB_OLD_SEL       cooperative-load transposes select with v_cndmask instead of v_bitop3
 //   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
 //   TG_AB_MAC_FLAT      cooperative MAC loads as flat_load (generic pointers) instead of global_load

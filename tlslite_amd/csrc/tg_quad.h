@@ -74,8 +74,20 @@ struct QuadAes {
         return (t0 ^ w) ^ quad_dpp<0x39>(t1);
 #else
         const uint32_t u = (t2 ^ k2) ^ quad_dpp<0x39>(t3);
+#ifdef TG_AB_FINAL_DPP
         const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
         return z ^ quad_dpp<0x4E>(u);
+#else
+        // the last step as v_mov_dpp of u + a plain 3-input XOR: a DPP instruction that reads
+        // a VGPR written by the instruction just before it (z) needs two wait states (s_nop 1),
+        // so the fused v_xor_b32_dpp put an s_nop on the round's critical path.  w is moved
+        // while the T0/T1 lookups are still in flight (the scheduling barrier keeps it there);
+        // bitop3 because a plain ^ would be folded back into v_xor_b32_dpp.
+        const uint32_t w = quad_dpp<0x4E>(u);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
+        return __builtin_amdgcn_bitop3_b32(z, w, z, 0x3C);
+#endif
 #endif
     }
     // per-lane round keys in the layout round()/last() expect: k[0] = whitening column q,
@@ -93,8 +105,15 @@ struct QuadAes {
         const uint32_t s0 = look<2, 0>(x) & 0xffu;
         const uint32_t s1 = look<3, 1>(x) & 0xff00u;
         const uint32_t u = (s2 ^ k) ^ quad_dpp<0x39>(s3);
+#ifdef TG_AB_FINAL_DPP
         const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
         return z ^ quad_dpp<0x4E>(u);
+#else
+        const uint32_t w = quad_dpp<0x4E>(u);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
+        return __builtin_amdgcn_bitop3_b32(z, w, z, 0x3C);
+#endif
     }
     // one block of one chain
     template <int NR>
