@@ -443,7 +443,11 @@ def main():
     if os.path.exists(tpath):
         try:
             pj = json.load(open(tpath))
-            if pj.get("dominant_kernel") == wl.dominant_kernel():
+            # kernel stems compared up to the first template argument (cbc_kernel<10> is the
+            # same kernel as cbc_kernel<10, false>: the second argument is the round's form)
+            def _key(k):
+                return (k or "").split(",")[0].rstrip(">")
+            if _key(pj.get("dominant_kernel")) == _key(wl.dominant_kernel()):
                 traffic = pj.get("hbm_bytes_per_launch")
                 seal_call_bytes = pj.get("seal_call_hbm_bytes")
         except Exception:

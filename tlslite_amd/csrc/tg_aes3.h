@@ -99,7 +99,6 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_MAC_PF        chunks the cooperative MAC loop prefetches (default 2)
 //   TG_AB_MAC_LB        mac_kernel's launch bound in 256-thread blocks per CU (default 3)
 //   TG_AB_OLD_ADDR      byte-1 T-table address by v_perm (as the other bytes) instead of v_bitop3
-//   TG_AB_FINAL_DPP     AES quad round's last XOR as v_xor_b32_dpp on z (s_nop on the critical path)
 //   TG_AB_OLD_SEL       cooperative-load transposes select with v_cndmask instead of v_bitop3
 //   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
 //   TG_AB_MAC_FLAT      cooperative MAC loads as flat_load (generic pointers) instead of global_load
@@ -415,7 +414,7 @@ __device__ __forceinline__ void st32t(uint8_t* p, uint32_t v) {
 // blocks b0+8..b0+15, then encrypt and store the 8 blocks.  CLAMP: the refill index is
 // clamped to the last block (the record's final groups); otherwise the 8 loads are one
 // base address + immediate offsets (fewer VGPRs and no per-block address arithmetic).
-template <int NR, bool AL, bool CLAMP>
+template <int NR, bool LAT, bool AL, bool CLAMP>
 __device__ __forceinline__ uint32_t cbc_group8(const QuadAes& aes, const uint32_t* k, uint32_t iv,
                                                const uint8_t* P, uint8_t* O, uint32_t b0, uint32_t last,
                                                uint32_t f[8]) {
@@ -436,7 +435,7 @@ __device__ __forceinline__ uint32_t cbc_group8(const QuadAes& aes, const uint32_
     uint8_t* Ob = O + 16 * b0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(c[i], iv, k[0], 0x96), k);
+        iv = aes.encrypt_w<NR, LAT>(__builtin_amdgcn_bitop3_b32(c[i], iv, k[0], 0x96), k);
         st32t<AL>(Ob + 16 * i, iv);
     }
     return iv;
@@ -449,7 +448,7 @@ __device__ __forceinline__ uint32_t cbc_group8(const QuadAes& aes, const uint32_
 // previous group's loads.  With the loop entered straight from the 8 prologue loads, the
 // merged header wait was vmcnt(1) -- every 8 blocks the wave waited for the previous
 // group's stores, which stalls the chain when HBM is loaded (the MAC phase's stream).
-template <int NR, bool AL>
+template <int NR, bool LAT, bool AL>
 __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t* k, uint32_t iv,
                                              const uint8_t* P, uint8_t* O, uint32_t nb) {
     if (nb == 0) return iv;
@@ -460,24 +459,26 @@ __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t*
     uint32_t b0 = 0;
     if (nb >= 16) {
         // groups whose refill (blocks b0+8..b0+15) lies inside the record
-        iv = cbc_group8<NR, AL, false>(aes, k, iv, P, O, 0, last, f);
-        for (b0 = 8; b0 + 16 <= nb; b0 += 8) iv = cbc_group8<NR, AL, false>(aes, k, iv, P, O, b0, last, f);
+        iv = cbc_group8<NR, LAT, AL, false>(aes, k, iv, P, O, 0, last, f);
+        for (b0 = 8; b0 + 16 <= nb; b0 += 8) iv = cbc_group8<NR, LAT, AL, false>(aes, k, iv, P, O, b0, last, f);
     }
     if (b0 + 8 <= nb) {  // the last full group: refill clamped
-        iv = cbc_group8<NR, AL, true>(aes, k, iv, P, O, b0, last, f);
+        iv = cbc_group8<NR, LAT, AL, true>(aes, k, iv, P, O, b0, last, f);
         b0 += 8;
     }
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         if (b0 + i < nb) {
-            iv = aes.encrypt_w<NR>(__builtin_amdgcn_bitop3_b32(f[i], iv, k[0], 0x96), k);
+            iv = aes.encrypt_w<NR, LAT>(__builtin_amdgcn_bitop3_b32(f[i], iv, k[0], 0x96), k);
             st32t<AL>(O + 16 * (b0 + i), iv);
         }
     }
     return iv;
 }
 
-template <int NR>
+// LAT: the few-chains (latency) form of the round, QuadAes::round; the launcher picks it
+// when a CU gets fewer chains than it has quads (cfg4), the throughput form otherwise
+template <int NR, bool LAT>
 __global__ void __launch_bounds__(C3_THREADS, 1)
 cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
            uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
@@ -523,19 +524,19 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
         uint8_t* B = wire + R.wire_off + 5;
         const bool al = (((uintptr_t)(pt + R.pt_off) | (uintptr_t)B) & 3) == 0;
         if (E) {
-            iv = aes.encrypt1<NR>(fiv ^ iv, k);
+            iv = aes.encrypt1<NR, LAT>(fiv ^ iv, k);
             st32(B + 4 * q, iv, al);
         }
         uint8_t* O = B + E + 4 * q;
         const uint32_t nb = n >> 4;
-        iv = al ? cbc_bulk<NR, true>(aes, k, iv, P, O, nb) : cbc_bulk<NR, false>(aes, k, iv, P, O, nb);
+        iv = al ? cbc_bulk<NR, LAT, true>(aes, k, iv, P, O, nb) : cbc_bulk<NR, LAT, false>(aes, k, iv, P, O, nb);
         // tail blocks from the MAC kernel's slot
         const uint32_t r16 = n & 15;
         const uint8_t* slot = tails + (size_t)r * TAIL_SLOT + 4 * q;
         uint8_t* Ot = B + E + (n - r16) + 4 * q;
         const uint32_t T = mt.tail_len;
         for (uint32_t off = 0; off < T; off += 16) {
-            iv = aes.encrypt1<NR>(*(const uint32_t*)(slot + off) ^ iv, k);
+            iv = aes.encrypt1<NR, LAT>(*(const uint32_t*)(slot + off) ^ iv, k);
             st32(Ot + off, iv, al);
         }
     }

@@ -382,7 +382,8 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
     } else {
         uint32_t cpw = (nchains + ncu - 1) / ncu;
         cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
-        auto kern = cbc_kernel<NR>;
+        // fewer chains than a workgroup's quads: the latency form of the AES round
+        auto kern = cpw < (uint32_t)C3_CHAINS ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
         hipError_t e = set_lds(kern, AES_LDS_BYTES);
         if (e != hipSuccess) return e;
         // persistent: at most one workgroup per CU, quads loop over chain generations

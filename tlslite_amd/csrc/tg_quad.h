@@ -61,34 +61,30 @@ struct QuadAes {
     // and the round key rides in that inner term: k2 is the key column of lane q+2 (round_keys()),
     // so once the T0/T1 lookups return only two dependent DPP XORs remain (a chain needs four).
     // The T2/T3 lookups are issued first: they feed the inner term.
+    // LAT (the few-chains regime, a lone wave per SIMD): the last step as v_mov_dpp of u +
+    // a plain 3-input XOR.  A DPP instruction that reads a VGPR written by the instruction
+    // just before it (z) needs two wait states, so the fused v_xor_b32_dpp puts an s_nop on
+    // the round's critical path; w is moved while the T0/T1 lookups are still in flight
+    // (the scheduling barrier keeps it there), and the XOR is a v_bitop3 because a plain ^
+    // would be folded back into v_xor_b32_dpp.  cfg4: 129.6 -> 125.9 ms.  With 16 waves
+    // per CU (cfg2, cfg3) the extra VALU instruction costs more than the latency it saves
+    // (cfg3 cipher phase 2.18 -> 2.24 ms), so the throughput form keeps the fused DPP.
+    template <bool LAT>
     __device__ __forceinline__ uint32_t round(uint32_t x, uint32_t k2) const {
         const uint32_t t2 = look<2, 2>(x);
         const uint32_t t3 = look<3, 3>(x);
         const uint32_t t0 = look<0, 0>(x);
         const uint32_t t1 = look<1, 1>(x);
-#ifdef TG_AB_ROUND_B
-        // one DPP XOR after the last lookup: ((k ^ dpp2 t2) ^ dpp3 t3) ^ t0 ^ dpp1 t1, with
-        // k2 = the key column of lane q+2 moved back by the first DPP (tools/build_ab.sh)
-        const uint32_t a = quad_dpp<0x4E>(t2 ^ k2);
-        const uint32_t w = a ^ quad_dpp<0x93>(t3);
-        return (t0 ^ w) ^ quad_dpp<0x39>(t1);
-#else
         const uint32_t u = (t2 ^ k2) ^ quad_dpp<0x39>(t3);
-#ifdef TG_AB_FINAL_DPP
-        const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
-        return z ^ quad_dpp<0x4E>(u);
-#else
-        // the last step as v_mov_dpp of u + a plain 3-input XOR: a DPP instruction that reads
-        // a VGPR written by the instruction just before it (z) needs two wait states (s_nop 1),
-        // so the fused v_xor_b32_dpp put an s_nop on the round's critical path.  w is moved
-        // while the T0/T1 lookups are still in flight (the scheduling barrier keeps it there);
-        // bitop3 because a plain ^ would be folded back into v_xor_b32_dpp.
-        const uint32_t w = quad_dpp<0x4E>(u);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
-        return __builtin_amdgcn_bitop3_b32(z, w, z, 0x3C);
-#endif
-#endif
+        if constexpr (!LAT) {
+            const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
+            return z ^ quad_dpp<0x4E>(u);
+        } else {
+            const uint32_t w = quad_dpp<0x4E>(u);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
+            return __builtin_amdgcn_bitop3_b32(z, w, z, 0x3C);
+        }
     }
     // per-lane round keys in the layout round()/last() expect: k[0] = whitening column q,
     // k[r >= 1] = column (q+2)&3 of round key r
@@ -98,6 +94,7 @@ struct QuadAes {
 #pragma unroll
         for (int r = 1; r <= NR; r++) k[r] = ek[4 * r + ((q + 2) & 3)];
     }
+    template <bool LAT>
     __device__ __forceinline__ uint32_t last(uint32_t x, uint32_t k) const {
         // S-box byte r sits at byte r of table (r+2)&3
         const uint32_t s2 = look<0, 2>(x) & 0xff0000u;
@@ -105,30 +102,30 @@ struct QuadAes {
         const uint32_t s0 = look<2, 0>(x) & 0xffu;
         const uint32_t s1 = look<3, 1>(x) & 0xff00u;
         const uint32_t u = (s2 ^ k) ^ quad_dpp<0x39>(s3);
-#ifdef TG_AB_FINAL_DPP
-        const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
-        return z ^ quad_dpp<0x4E>(u);
-#else
-        const uint32_t w = quad_dpp<0x4E>(u);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
-        return __builtin_amdgcn_bitop3_b32(z, w, z, 0x3C);
-#endif
+        if constexpr (!LAT) {
+            const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
+            return z ^ quad_dpp<0x4E>(u);
+        } else {
+            const uint32_t w = quad_dpp<0x4E>(u);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
+            return __builtin_amdgcn_bitop3_b32(z, w, z, 0x3C);
+        }
     }
     // one block of one chain
-    template <int NR>
+    template <int NR, bool LAT>
     __device__ __forceinline__ uint32_t encrypt1(uint32_t a, const uint32_t* ka) const {
         a ^= ka[0];
 #pragma unroll
-        for (int r = 1; r < NR; r++) a = round(a, ka[r]);
-        return last(a, ka[NR]);
+        for (int r = 1; r < NR; r++) a = round<LAT>(a, ka[r]);
+        return last<LAT>(a, ka[NR]);
     }
     // one block whose input is already whitened (x = block ^ k[0])
-    template <int NR>
+    template <int NR, bool LAT>
     __device__ __forceinline__ uint32_t encrypt_w(uint32_t a, const uint32_t* ka) const {
 #pragma unroll
-        for (int r = 1; r < NR; r++) a = round(a, ka[r]);
-        return last(a, ka[NR]);
+        for (int r = 1; r < NR; r++) a = round<LAT>(a, ka[r]);
+        return last<LAT>(a, ka[NR]);
     }
 };
 

@@ -144,13 +144,13 @@ __global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict_
             for (int r = 1; r < NR; r++) {
                 uint32_t y[ILP];
 #pragma unroll
-                for (int i = 0; i < ILP; i++) y[i] = LAYOUT == 4 ? L.round(x[i], k[r]) : L.round_b(x[i], k[r]);
+                for (int i = 0; i < ILP; i++) y[i] = LAYOUT == 4 ? L.template round<false>(x[i], k[r]) : L.round_b(x[i], k[r]);
 #pragma unroll
                 for (int i = 0; i < ILP; i++) x[i] = y[i];
             }
             uint32_t y[ILP];
 #pragma unroll
-            for (int i = 0; i < ILP; i++) y[i] = LAYOUT == 4 ? L.last(x[i], k[NR]) : L.last_b(x[i], k[NR]);
+            for (int i = 0; i < ILP; i++) y[i] = LAYOUT == 4 ? L.template last<false>(x[i], k[NR]) : L.last_b(x[i], k[NR]);
 #pragma unroll
             for (int i = 0; i < ILP; i++) x[i] = y[i];
         }

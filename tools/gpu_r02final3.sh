@@ -1,10 +1,10 @@
 #!/bin/bash
-# r02final2: the final round-2 tree on one MI355X -- full GPU tests, smoke, every bench
+# r02final3: the final round-2 tree on one MI355X -- full GPU tests, smoke, every bench
 # config, a 2-rank torchrun of bench.py (both ranks on this box's one GPU), and rocprofv3
 # kernel-trace statistics of each config.  Stops at the first failure.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r02final2
+O=$R/gpurun_out/r02final3
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }
