@@ -40,6 +40,13 @@ constexpr uint32_t TAIL_SLOT = 64;
 #endif
 constexpr int C3_THREADS = 64 * TG_AB_CBC_WAVES;  // 16 cipher waves
 constexpr int C3_CHAINS = 16 * TG_AB_CBC_WAVES;
+// Many-chains regime (more chains than one generation of 16-wave workgroups, cfg3): 12
+// cipher waves per CU and the MAC kernel at <= 128 VGPRs with a one-chunk prefetch, so that
+// two MAC waves fit per SIMD beside three cipher waves (3 x 80 + 2 x 128 <= 512): the MAC
+// phase is that regime's critical path (cfg3 +2 %, same-box A/B; cfg2, one generation,
+// keeps 16 cipher waves: -23 % with 12)
+constexpr int C3_WAVES_MANY = 12;
+constexpr int MAC_LB_MANY = 4, MAC_PF_MANY = 1;
 
 template <int CIPHER_ID, int MAC, bool SSL3>
 __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
@@ -101,6 +108,7 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_OLD_ADDR      byte-1 T-table address by v_perm (as the other bytes) instead of v_bitop3
 //   TG_AB_OLD_SEL       cooperative-load transposes select with v_cndmask instead of v_bitop3
 //   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
+//   TG_AB_NO_MANY       no many-chains configuration (12 cipher waves + 128-VGPR MAC kernel, cfg3)
 //   TG_AB_MAC_FLAT      cooperative MAC loads as flat_load (generic pointers) instead of global_load
 //   TG_AB_DES_ANDOR     3DES SP-box address by v_and_or_b32 instead of v_bitop3
 //   TG_AB_OPEN_QUAD     AES open decrypt on the quad layout (open_dec_kernel, round 1) instead of
@@ -224,7 +232,7 @@ __device__ __forceinline__ void quad_transpose4(uint32_t x[4], uint32_t q) {
 // chunk, ~8 % of a SHA-1 block) hand every lane its own record's 16 words.  The quad walks
 // its longest record; a lane compresses only its own chunks and loads never leave a
 // record (chunk index clamped to the record's last one).  Needs nfull >= 1 in every lane.
-template <class M>
+template <int PF, class M>
 __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t nfull, uint32_t q) {
     uint32_t nmax = max(nfull, quad_dpp<0xB1>(nfull));
     nmax = max(nmax, quad_dpp<0x4E>(nmax));
@@ -236,11 +244,11 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
     NL[L] = quad_lane<L>(nfull) - 1;
     TG_QL(0) TG_QL(1) TG_QL(2) TG_QL(3)
 #undef TG_QL
-    // prefetch ring of MAC_PF chunks: under the cipher phase's HBM traffic a load takes longer
+    // prefetch ring of PF chunks: under the cipher phase's HBM traffic a load takes longer
     // than one chunk's compression
-    uint4 nxt[MAC_PF][4];
+    uint4 nxt[PF][4];
 #pragma unroll
-    for (int d = 0; d < MAC_PF; d++)
+    for (int d = 0; d < PF; d++)
 #pragma unroll
         for (int L = 0; L < 4; L++) {
 #ifdef TG_AB_MAC_NOLOAD
@@ -254,15 +262,15 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
 #pragma unroll
         for (int L = 0; L < 4; L++) cur[L] = nxt[0][L];
 #pragma unroll
-        for (int d = 0; d + 1 < MAC_PF; d++)
+        for (int d = 0; d + 1 < PF; d++)
 #pragma unroll
             for (int L = 0; L < 4; L++) nxt[d][L] = nxt[d + 1][L];
 #ifdef TG_AB_MAC_NOLOAD
 #pragma unroll
-        for (int L = 0; L < 4; L++) nxt[MAC_PF - 1][L] = make_uint4(cur[L].y + c, cur[L].z ^ c, cur[L].w, cur[L].x);
+        for (int L = 0; L < 4; L++) nxt[PF - 1][L] = make_uint4(cur[L].y + c, cur[L].z ^ c, cur[L].w, cur[L].x);
 #else
 #pragma unroll
-        for (int L = 0; L < 4; L++) nxt[MAC_PF - 1][L] = ldg16(PL[L] + 64 * min(c + MAC_PF, NL[L]));
+        for (int L = 0; L < 4; L++) nxt[PF - 1][L] = ldg16(PL[L] + 64 * min(c + PF, NL[L]));
 #endif
         // component t of lane p's piece of record L = record L's word 4p + t
         uint32_t d[16], x[4];
@@ -297,8 +305,8 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
 #ifndef TG_AB_MAC_LB
 #define TG_AB_MAC_LB 3
 #endif
-template <int MAC, bool SSL3, int BS = 16>
-__global__ void __launch_bounds__(256, TG_AB_MAC_LB) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
+template <int MAC, bool SSL3, int BS = 16, int LB = TG_AB_MAC_LB, int PF = MAC_PF>
+__global__ void __launch_bounds__(256, LB) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
                                                  const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
                                                  const ConnState* __restrict__ states, int32_t* __restrict__ wire_len,
                                                  const RecMeta* __restrict__ meta, uint8_t* __restrict__ tails,
@@ -334,7 +342,7 @@ __global__ void __launch_bounds__(256, TG_AB_MAC_LB) mac_kernel(const tlsgpu_rec
     coop &= quad_dpp<0x4E>(coop);
 #ifndef TG_AB_NO_MAC
     if (coop) {
-        mac_bulk_coop(mac, P, nfull, threadIdx.x & 3u);
+        mac_bulk_coop<PF>(mac, P, nfull, threadIdx.x & 3u);
     } else if (act) {
         if (al16) mac_bulk<true>(mac, P, nfull);
         else mac_bulk<false>(mac, P, nfull);
@@ -478,8 +486,8 @@ __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t*
 
 // LAT: the few-chains (latency) form of the round, QuadAes::round; the launcher picks it
 // when a CU gets fewer chains than it has quads (cfg4), the throughput form otherwise
-template <int NR, bool LAT>
-__global__ void __launch_bounds__(C3_THREADS, 1)
+template <int NR, bool LAT, int WAVES = TG_AB_CBC_WAVES>
+__global__ void __launch_bounds__(64 * WAVES, 1)
 cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
            uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
            ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,

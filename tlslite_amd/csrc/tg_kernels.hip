@@ -344,6 +344,16 @@ __global__ void fill_kernel(uint8_t* __restrict__ p, size_t bytes, uint64_t seed
 // ---------------------------------------------------------------- seal launchers
 size_t seal_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * (sizeof(RecMeta) + TAIL_SLOT); }
 
+// AES batches with more chains than one generation of 16-wave cipher workgroups: the
+// many-chains configuration (C3_WAVES_MANY cipher waves, MAC kernel at MAC_LB_MANY)
+static bool many_chains(uint32_t nchains) {
+#ifdef TG_AB_NO_MANY
+    return false;
+#else
+    return nchains > (uint32_t)C3_CHAINS * cu_count();
+#endif
+}
+
 // phase 1 (stream s1): meta memset + seqnum prefix + per-record MAC / tail / header.
 // NR 0 = 3DES (8-byte blocks)
 template <int NR, int MAC, bool SSL3>
@@ -358,8 +368,12 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((prefix_kernel<CID, MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains,
                        recs, states, wire_len, meta, nrecords, epoch);
-    hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS>), dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords, pt,
-                       wire, states, wire_len, meta, tails, epoch);
+    if (NR != 0 && many_chains(nchains))
+        hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS, MAC_LB_MANY, MAC_PF_MANY>), dim3((nrecords + 255) / 256), dim3(256),
+                           0, s, recs, nrecords, pt, wire, states, wire_len, meta, tails, epoch);
+    else
+        hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS>), dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords,
+                           pt, wire, states, wire_len, meta, tails, epoch);
     return hipGetLastError();
 }
 
@@ -380,17 +394,20 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
                            nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch);
         return hipGetLastError();
     } else {
+        const bool many = many_chains(nchains);
+        const uint32_t wg_chains = many ? 16u * C3_WAVES_MANY : (uint32_t)C3_CHAINS;
         uint32_t cpw = (nchains + ncu - 1) / ncu;
-        cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
+        cpw = cpw < 1 ? 1 : (cpw > wg_chains ? wg_chains : cpw);
         // fewer chains than a workgroup's quads: the latency form of the AES round
-        auto kern = cpw < (uint32_t)C3_CHAINS ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
+        auto kern = many ? cbc_kernel<NR, false, C3_WAVES_MANY>
+                         : cpw < (uint32_t)C3_CHAINS ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
         hipError_t e = set_lds(kern, AES_LDS_BYTES);
         if (e != hipSuccess) return e;
         // persistent: at most one workgroup per CU, quads loop over chain generations
         uint32_t grid = (nchains + cpw - 1) / cpw;
         grid = grid > ncu ? ncu : grid;
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(C3_THREADS), AES_LDS_BYTES, s, chains, nchains, recs, nrecords, pt,
-                           wire, states, meta, tails, cpw, epoch);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(many ? 64 * C3_WAVES_MANY : C3_THREADS), AES_LDS_BYTES, s, chains,
+                           nchains, recs, nrecords, pt, wire, states, meta, tails, cpw, epoch);
         return hipGetLastError();
     }
 }
