@@ -45,7 +45,10 @@ constexpr int C3_CHAINS = 16 * TG_AB_CBC_WAVES;
 // two MAC waves fit per SIMD beside three cipher waves (3 x 80 + 2 x 128 <= 512): the MAC
 // phase is that regime's critical path (cfg3 +2 %, same-box A/B; cfg2, one generation,
 // keeps 16 cipher waves: -23 % with 12)
-constexpr int C3_WAVES_MANY = 12;
+#ifndef TG_AB_WAVES_MANY
+#define TG_AB_WAVES_MANY 12
+#endif
+constexpr int C3_WAVES_MANY = TG_AB_WAVES_MANY;
 constexpr int MAC_LB_MANY = 4, MAC_PF_MANY = 1;
 
 template <int CIPHER_ID, int MAC, bool SSL3>
@@ -109,6 +112,7 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_OLD_SEL       cooperative-load transposes select with v_cndmask instead of v_bitop3
 //   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
 //   TG_AB_NO_MANY       no many-chains configuration (12 cipher waves + 128-VGPR MAC kernel, cfg3)
+//   TG_AB_WAVES_MANY    cipher waves per CU in the many-chains configuration (default 12)
 //   TG_AB_MAC_FLAT      cooperative MAC loads as flat_load (generic pointers) instead of global_load
 //   TG_AB_DES_ANDOR     3DES SP-box address by v_and_or_b32 instead of v_bitop3
 //   TG_AB_OPEN_QUAD     AES open decrypt on the quad layout (open_dec_kernel, round 1) instead of
