@@ -8,8 +8,11 @@ TLS-record seal of 64 Ki x 16 KiB records (config 2), in plaintext GiB/s.
 A step = one seal of the whole per-GPU batch (every record MAC'd, padded,
 CBC-encrypted and framed; connection states carried from the previous step).
 Multi-GPU is weak scaling: each rank owns its own batch on its own device
-(connection sharding, no collective on the data path); torch.distributed (gloo)
-is only used for the start/stop barriers and the max-over-ranks time.
+(connection sharding, no collective on the data path); the ranks meet only for
+the start/stop barriers and the max-over-ranks time (tlslite_amd.shard: a small
+TCP rendezvous, no PyTorch).  After the timed loop the same number of seals is
+replayed sequentially from the initial states and the last step's wire arena,
+wire lengths and final states are compared (`timed_bit_exact`).
 
 Prints ONE JSON line (rank 0) with roofline + cpu_baseline objects.
 """
@@ -341,16 +344,39 @@ def derive_rate(stream, nconn=4096, steps=10):
                       "HMAC-SHA1 midstates, one lane per connection; median of HIP-event-timed calls"}
 
 
+def copy_rate(wl, stream, reps=5):
+    """HBM copy rate of this GPU (GB/s, read + write bytes): device-to-device copies of
+    the wire arena, HIP events on one stream, best of `reps` -- what a kernel that only
+    streams its bytes could reach (the fraction of the measured copy rate
+    beside the 8 TB/s spec fraction)."""
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import DeviceBuffer, Event
+    n = min(wl.wire_bytes, 1 << 30)
+    dst = DeviceBuffer(n)
+    best = None
+    for _ in range(reps):
+        a, b = Event(), Event()
+        a.record(stream)
+        N.call("tlsgpu_memcpy_d2d", dst.ptr, wl.d_wire.ptr, n, stream.handle)
+        b.record(stream)
+        stream.synchronize()
+        ms = a.elapsed_ms(b)
+        best = ms if best is None or ms < best else best
+    dst.free()
+    return 2.0 * n / (best / 1e3) / 1e9
+
+
 def main():
     args = parse()
-    from tlslite_amd.shard import ShardGroup
-    D = ShardGroup("gloo")
+    from tlslite_amd.shard import ShardGroup, device_for_rank
+    D = ShardGroup()
     from tlslite_amd import _native as N
     from tlslite_amd.device import Event, Stream, set_device, synchronize, device_count, arch
     if device_count() < 1:
         raise SystemExit("bench.py: no GPU visible to libtlsgpu.so")
-    set_device(D.local % device_count())
-    dev_arch = arch(D.local % device_count())
+    dev = device_for_rank(D.local, device_count())
+    set_device(dev)
+    dev_arch = arch(dev)
     wl = build_workload(args.config, D.rank, D.world, args.records)
     stream = Stream()
     wl.to_device(stream)
@@ -378,6 +404,7 @@ def main():
         wl.reset_states(stream)
         stream.synchronize()
 
+    n_state_launches = 0  # seals applied to the connection states since the last reset
     # ---- one-call latency (no overlap between calls): seal_dev on one stream
     nlat = min(args.steps, 10)
     ev = [Event() for _ in range(nlat + 1)]
@@ -388,6 +415,7 @@ def main():
         wl.launch([stream])
         ev[k + 1].record(stream)
     stream.synchronize()
+    n_state_launches += 1 + nlat
     call_ms = float(np.mean([ev[k].elapsed_ms(ev[k + 1]) for k in range(nlat)]))
 
     # ---- warmup + timed region: successive batches through the seal pipeline
@@ -396,6 +424,7 @@ def main():
     pipe = SealPipeline(wl.n_records)
     for _ in range(args.warmup):
         wl.launch(pipeline=pipe)
+    n_state_launches += args.warmup
     pipe.synchronize()
     synchronize()
     D.barrier()
@@ -408,6 +437,7 @@ def main():
     if conc:
         for _ in range(args.warmup):
             wl.launch(conc)
+        n_state_launches += args.warmup
         for s_ in conc:
             s_.synchronize()
     t0 = time.perf_counter()
@@ -425,8 +455,24 @@ def main():
     synchronize()
     wall = time.perf_counter() - t0
     D.barrier()
+    n_state_launches += args.steps
     per_launch = [a.elapsed_ms(b) for a, b in kev]
     pipe.close()
+
+    # ---- the timed output itself: replay the same number of seals one call at a time
+    # (tlsgpu_seal_dev, one stream) from the initial states; the last step's wire arena,
+    # wire lengths and the final states must equal the pipelined / concurrent run's
+    timed_ok = None
+    if not args.no_check:
+        got = (wl.d_wire.download(), wl.d_len.download(), wl.d_states.download())
+        wl.reset_states(stream)
+        for _ in range(n_state_launches):
+            wl.launch([stream])
+        stream.synchronize()
+        ok = (np.array_equal(got[0], wl.d_wire.download()) and np.array_equal(got[1], wl.d_len.download())
+              and np.array_equal(got[2], wl.d_states.download()))
+        del got
+        timed_ok = D.sum(0.0 if ok else 1.0) == 0.0
     t_max = D.max(wall)
     total_pt = D.sum(wl.plaintext_total * args.steps)
     value = total_pt / GIB / t_max
@@ -434,8 +480,11 @@ def main():
     # roofline of the dominant kernel (the CBC kernel for AES suites; the single
     # seal kernel otherwise), timed with events on the stream it runs on
     avg_ms = float(np.mean(per_launch))
-    alg_bytes = wl.plaintext_total + wl.wire_total  # read P + write 5+C per record
+    # read P + write 5+C per record of the records the timed kernel seals: the
+    # whole batch, or in a mixed batch (cfg5) the first launch's variant (its 3DES leg)
+    alg_bytes = wl.launch_alg_bytes[0]
     achieved = alg_bytes / (avg_ms / 1e3) / 1e9
+    copy_gbs = copy_rate(wl, stream)
     # HBM bytes per launch of the same kernel from the committed PMC summary
     # (tools/pmc_kernels.sh -> profiles/pmc_<cfg>.json), only when it names this kernel
     traffic = seal_call_bytes = None
@@ -453,7 +502,7 @@ def main():
         except Exception:
             traffic = seal_call_bytes = None
     state_bytes = wl.cipher_state_bytes()
-    lookups = wl.aes_lookups() if wl.dominant_kernel().startswith(("cbc_kernel", "lseal_kernel")) else None
+    lookups = wl.aes_lookups() if wl.dominant_kernel().startswith(("cbc_kernel", "cbc_pair_kernel")) else None
     lds = None
     if lookups:
         g = lookups / (avg_ms / 1e3) / 1e9
@@ -508,6 +557,11 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": wl.dominant_kernel(), "kernel_avg_ms": round(avg_ms, 4),
                          "alg_bytes_per_launch": alg_bytes,
+                         "batch_alg_bytes": wl.plaintext_total + wl.wire_total,
+                         "copy_measured": round(copy_gbs, 1),
+                         "frac_of_copy": round(achieved / copy_gbs, 4),
+                         "copy_note": "device-to-device copy of the wire arena on this GPU, (read + write) "
+                                      "bytes / HIP-event time, best of 5: the practical HBM ceiling",
                          "traffic_ratio": round(traffic / alg_bytes, 3) if traffic else None,
                          "state_bytes_per_launch": state_bytes,
                          "traffic_ratio_with_state": round(traffic / (alg_bytes + state_bytes), 3) if traffic else None,
@@ -521,6 +575,9 @@ def main():
             "ms_per_seal_call": round(call_ms, 4),
             "cpu_baseline": cpu,
             "bit_exact": bit_exact,
+            "timed_bit_exact": timed_ok,
+            "timed_check": "the %d seals before the last step's output replayed one call at a time from the "
+                           "initial states: last wire arena, wire lengths and final states equal" % n_state_launches,
             "host_inclusive": host_inc,
             "open": open_res,
             "derive": derive_res,

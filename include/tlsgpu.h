@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TLSGPU_ABI_VERSION 2
+#define TLSGPU_ABI_VERSION 3
 
 /* ---- suite components (tlsrecordlayer.py:1063-1095, constants.py:159-201) */
 enum {
@@ -170,6 +170,8 @@ int tlsgpu_get_device(int *ordinal);
 int tlsgpu_device_synchronize(void);
 /* fills *name (cap bytes) with the device arch name, e.g. "gfx950" */
 int tlsgpu_device_arch(int ordinal, char *name, size_t cap);
+/* compute units of device `ordinal` (the seal kernels size their layouts per CU) */
+int tlsgpu_device_cu_count(int ordinal, int *n);
 
 /* ---- memory ------------------------------------------------------------- */
 int tlsgpu_malloc(void **dptr, size_t bytes);
@@ -224,16 +226,18 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state *st, uint32_t pt_len, uint32_t 
  * tlsgpu_seal_dev, or pass NULL there to use a library-owned workspace, one
  * per (device, stream): calls on different streams never share one. */
 size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords);
+/* Free every library-owned seal / open workspace (the NULL-workspace buffers, one per
+ * (device, stream) ever used).  Waits for each device they live on first.  Callers that
+ * create and destroy many streams call it; otherwise the buffers live until exit. */
+int tlsgpu_release_workspaces(void);
+/* Name of the cipher-phase kernel a seal call of `nchains` chains of `variant` runs on the
+ * current device (its rocprofv3 name stem, e.g. "cbc_kernel<10, false>"): the layout is
+ * chosen from the chains per CU.  Diagnostics / profiling only. */
+int tlsgpu_seal_cipher_kernel(uint32_t variant, uint32_t nchains, char *name, size_t cap);
 int tlsgpu_seal_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_record *records,
                     uint32_t nrecords, const uint8_t *pt, uint8_t *wire, tlsgpu_conn_state *states,
                     int32_t *wire_len, uint32_t variant, void *workspace, size_t workspace_bytes,
                     tlsgpu_stream s);
-/* AES suites: from this many chains per call on the current device, the seal runs one
- * lane per chain with the MAC and the CBC of each record in the same lane; below it, the
- * MAC of every record runs in parallel and each chain's CBC on four lanes.  The layouts
- * give identical bytes.  UINT32_MAX: this build has only the split layout (the product
- * library; the lane layout is an A/B build). */
-int tlsgpu_seal_lane_min_chains(uint32_t *nchains);
 /* ---- seal pipeline: successive tlsgpu_pipeline_seal calls overlap the MAC
  * phase of call k+1 with the cipher phase of call k (AES suites; two
  * library-owned streams, three workspaces in rotation, so the MAC phase may run
@@ -264,6 +268,11 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain *chains, uint32_t
  * record offsets of the next sub-batch, so records should be laid out in chain
  * order (as tlsgpu_seal_dev callers normally do); any other layout is sealed as
  * one sub-batch.  Synchronous: wire_host and wire_len_host are complete on return.
+ * Every record's wire slot must hold its sealed size (header, [explicit IV], P, MAC,
+ * padding): an RC4 record that would not fit fails the call with TLSGPU_EINVAL; a CBC
+ * record (whose size depends on the state's version) gets wire_len = TLSGPU_EINVAL and is
+ * not sealed (no seqnum consumed).  Bytes of wire_host between records are written as
+ * zeros.
  * wire_len_host: nrecords int32 (as tlsgpu_seal_dev's wire_len). */
 typedef struct tlsgpu_host_pipeline_s *tlsgpu_host_pipeline;
 int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline *p, size_t chunk_bytes, int depth);

@@ -50,3 +50,9 @@ def load_golden():
         with open(PATH) as f:
             _cache = json.load(f)["cases"]
     return _cache
+
+
+def load_json(name):
+    """Another committed fixture under tests/golden/ (sessions.json, batches.json, ...)."""
+    with open(os.path.join(os.path.dirname(PATH), name)) as f:
+        return json.load(f)

@@ -65,7 +65,9 @@ def test_hip_matches_reference_batch(name):
     wl.launch()
     synchronize()
     wire = wl.d_wire.download()
-    assert _wire_digest(wl, wire, wl.wire_len) == b["wire_sha256"]
+    d_len = wl.d_len.download().view(np.int32)  # the device's own wire_len output
+    assert d_len.tolist() == wl.wire_len.astype(np.int32).tolist()
+    assert _wire_digest(wl, wire, d_len) == b["wire_sha256"]
     st = device_states(wl)
     assert _state_digest(wl, lambda c: st[c].seqnum, lambda c: st[c].iv, lambda c: st[c].rc4) == b["state_sha256"]
     wl.free()

@@ -117,13 +117,14 @@ def _mixed_workload(n, pt_len, seed, suites=("AES128-SHA", "RC4-SHA")):
     return W.Workload("mixed", groups, seed, rec_order=rng.permutation(3 * n))
 
 
-@pytest.mark.parametrize("kind", ["cfg2", "mixed", "3des", "rc4_3des", "lane"])
+@pytest.mark.parametrize("kind", ["cfg2", "mixed", "3des", "rc4_3des", "many"])
 def test_pipeline_equals_sequential(kind):
     """tlsgpu_pipeline_seal: K successive batches (MAC phase of batch k+1
     overlapping the cipher phase of batch k) give the same wire bytes and final
     connection states as K sequential tlsgpu_seal_dev calls -- for AES, the
     3DES split path (prefix / MAC / tdes4_kernel), RC4 + 3DES mixes, and AES
-    batches large enough for the lane kernel (tg_lane.h)."""
+    batches with more chains than one cipher-workgroup generation per CU (the
+    throughput layout, tlsgpu_seal_cipher_kernel)."""
     _T()
     from tlslite_amd import workloads as W
     from tlslite_amd.device import DeviceBuffer, Stream
@@ -137,10 +138,7 @@ def test_pipeline_equals_sequential(kind):
     elif kind == "rc4_3des":
         wl = _mixed_workload(300, 1999, 14, ("3DES-SHA", "RC4-SHA"))
     else:
-        from tlslite_amd.recordlayer import seal_lane_min_chains
-        if seal_lane_min_chains() == 0xffffffff:
-            pytest.skip("lane layout not in this build (A/B build TG_AB_LANE_SEAL, DESIGN.md §3.7)")
-        wl = W.cfg3(n=seal_lane_min_chains() + 1000, pt_len=300, seed=15)
+        wl = W.cfg3(n=_many_chains() + 1000, pt_len=300, seed=15)
     wl.to_device()
     K = 4
     s = Stream()
@@ -287,14 +285,15 @@ def test_unaligned_arenas_vs_oracle(pt_shift, wire_shift, suite, version):
         assert s.seqnum == o.seqnum
 
 
-@pytest.mark.parametrize("kind", ["cfg2", "chained", "shuffled"])
+@pytest.mark.parametrize("kind", ["cfg2", "chained", "shuffled", "rc4", "3des"])
 @pytest.mark.parametrize("pinned", [True, False])
 def test_host_pipeline_equals_device_path(kind, pinned):
     """tlsgpu_host_pipeline_seal (records in host memory; sub-batches' H2D, seal and
     D2H overlapped on 3 streams, pageable buffers staged through pinned ones) gives
     the same wire arena, wire lengths and final states as the device-resident
     tlsgpu_seal_dev path -- with a small chunk so the batch is cut into many
-    sub-batches, and for a shuffled arena layout (one sub-batch)."""
+    sub-batches, for a shuffled arena layout (one sub-batch), and for the RC4
+    single-kernel branch and the 3DES split path (TLS 1.0 and 1.2 records)."""
     _T()
     from tlslite_amd import workloads as W
     from tlslite_amd.constants import ContentType
@@ -304,6 +303,9 @@ def test_host_pipeline_equals_device_path(kind, pinned):
         wl = W.cfg2(n=700, pt_len=5003, seed=21)
     elif kind == "chained":
         wl = W.cfg4(nconn=40, recs_per_conn=5, pt_len=3001, seed=22)
+    elif kind in ("rc4", "3des"):
+        suites = ("RC4-SHA", "RC4-SHA") if kind == "rc4" else ("3DES-SHA", "3DES-SHA")
+        wl = W.Workload(kind, _mixed_workload(200, 4001, 24, suites).groups, 24)
     else:
         g = W.cfg2(n=300, pt_len=777, seed=23).groups
         wl = W.Workload("shuffled", g, 23, rec_order=np.random.default_rng(23).permutation(300))
@@ -337,22 +339,83 @@ def test_host_pipeline_equals_device_path(kind, pinned):
     wl.free()
 
 
+@pytest.mark.parametrize("suite", ["AES128-SHA", "RC4-SHA"])
+def test_host_pipeline_undersized_wire_arena(suite):
+    """A wire arena one byte shorter than the last record's sealed form: the kernels
+    must not write past it.  A CBC record's size depends on the state's version (device
+    state), so that record alone is refused (wire_len = TLSGPU_EINVAL, nothing written,
+    its state untouched) and the others are sealed; RC4 sizes are known on the host, so
+    the call fails with TLSGPU_EINVAL before anything runs."""
+    T = _T()
+    from tlslite_amd import _native as N
+    from tlslite_amd import workloads as W
+    from tlslite_amd.constants import ContentType
+    from tlslite_amd.device import synchronize
+    from tlslite_amd.recordlayer import HostSealPipeline, make_chains, make_records
+    from oracle import oracle as O
+    rng = np.random.default_rng(25)
+    _, kl, ivl, _, ml = O.SUITES[suite]
+    ivs = np.frombuffer(rng.bytes(ivl * 64), dtype=np.uint8).reshape(64, ivl) if ivl else None
+    g = W.Group(suite, (3, 3) if ivl else (3, 1), [rng.bytes(kl)], ivs, [rng.bytes(ml)],
+                [rng.bytes(ivl)] if ivl else None, np.arange(64, dtype=np.uint64), 1, 3001)
+    wl = W.Workload(suite, [g], 25)  # one record per connection
+    wl.to_device()
+    wl.launch()
+    synchronize()
+    ref_wire, ref_states = wl.d_wire.download(), wl.d_states.download()
+    var = wl.launches[0][0]
+    recs = make_records(wl.pt_off, wl.wire_off, wl.pt_len, ContentType.application_data, 0)
+    chains = make_chains(np.arange(wl.n_chains, dtype=np.uint32), wl.chain_first, wl.chain_count)
+    last = int(np.argmax(wl.wire_off))
+    end = int(wl.wire_off[last]) + int(wl.wire_len[last])
+    pt_h = wl.d_pt.download()
+    wire_h = np.zeros(end - 1, dtype=np.uint8)
+    lens = np.zeros(wl.n_records, dtype=np.int32)
+    wl.reset_states()
+    synchronize()
+    with HostSealPipeline(chunk_bytes=64 << 10, depth=2) as hp:
+        if suite.startswith("RC4"):
+            with pytest.raises(N.TLSGPUError) as ei:
+                hp.seal(chains, recs, pt_h, wire_h, wl.d_states, lens, var)
+            assert ei.value.code == N.EINVAL
+            assert not wire_h.any()
+            return
+        hp.seal(chains, recs, pt_h, wire_h, wl.d_states, lens, var)
+    want = wl.wire_len.astype(np.int32).copy()
+    want[last] = N.EINVAL
+    assert lens.tolist() == want.tolist()
+    assert np.array_equal(wire_h[:int(wl.wire_off[last])], ref_wire[:int(wl.wire_off[last])])
+    assert not wire_h[int(wl.wire_off[last]):].any()  # the refused record: nothing written
+    st = wl.d_states.download().reshape(-1, N.CONN_STATE_BYTES)
+    ref = ref_states.reshape(-1, N.CONN_STATE_BYTES)
+    init = wl.host_states().reshape(-1, N.CONN_STATE_BYTES)
+    owner = int(np.searchsorted(wl.chain_first.astype(np.int64), last, side="right")) - 1
+    for c in range(wl.n_chains):
+        assert np.array_equal(st[c], init[c] if c == owner else ref[c]), c
+    wl.free()
+
+
+def _many_chains():
+    """Chains per call from which the cipher phase runs its throughput layout on every
+    CU (a full 256-chain workgroup per CU and more: cfg2 / cfg3 shapes)."""
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import cu_count
+    return 256 * cu_count()
+
+
 @pytest.mark.parametrize("suite,version", [("AES256-SHA256", (3, 3)), ("AES128-SHA", (3, 1)), ("AES128-SHA", (3, 0)),
                                            ("AES256-SHA", (3, 2))])
-def test_lane_path_vs_oracle(suite, version):
-    """A seal call of at least tlsgpu_seal_lane_min_chains() chains runs on the lane
-    kernel (tg_lane.h: one lane per chain, MAC and CBC of a record in the same lane;
-    an A/B build, TLSGPU_LIB=tools/ab/lane/libtlsgpu.so -- skipped on the product library).
-    One launch of that many chains plus a persistent second generation -- one-record
-    connections of 1,434 B (cfg3's record), 3-record chains of 100 B, 2-record chains of
-    5,003 B, chains of sub-block, block-sized and empty records, random content types and
-    badMAC / badPadding faults on ~3 % of the records -- equals the oracle byte for byte,
-    every wire length, and every chain's final CBC residue and seqnum
-    (tlsrecordlayer.py:538-617, python_aes.py:44)."""
+def test_many_chains_vs_oracle(suite, version):
+    """A seal call with more chains than one cipher-workgroup generation per CU (the
+    layout cfg2 / cfg3 run, tlsgpu_seal_cipher_kernel names it) plus a persistent second
+    generation -- one-record connections of 1,434 B (cfg3's record), 3-record chains of
+    100 B, 2-record chains of 5,003 B, chains of sub-block, block-sized and empty
+    records, random content types and badMAC / badPadding faults on ~3 % of the records
+    -- equals the oracle byte for byte, every wire length, and every chain's final CBC
+    residue and seqnum (tlsrecordlayer.py:538-617, python_aes.py:44)."""
     _T()
     from tlslite_amd import workloads as W
     from tlslite_amd.device import synchronize
-    from tlslite_amd.recordlayer import seal_lane_min_chains
     from tests.wl_oracle import device_states, oracle_seal
     from oracle import oracle as O
     rng = np.random.default_rng(zlib.crc32(repr(("lane", suite, version)).encode()))
@@ -362,9 +425,7 @@ def test_lane_path_vs_oracle(suite, version):
         ivs = np.frombuffer(rng.bytes(ivl * nconn), dtype=np.uint8).reshape(nconn, ivl)
         return W.Group(suite, version, [rng.bytes(kl)], ivs, [rng.bytes(ml)], [rng.bytes(ivl)],
                        rng.integers(0, 2 ** 40, nconn, dtype=np.uint64), recs, n)
-    nmin = seal_lane_min_chains()
-    if nmin == 0xffffffff:
-        pytest.skip("lane layout not in this build (A/B build TG_AB_LANE_SEAL, DESIGN.md §3.7)")
+    nmin = _many_chains()
     small = [grp(20000, 3, 100), grp(6000, 2, 5003), grp(3000, 2, 0), grp(3000, 4, 15), grp(3000, 1, 16),
              grp(3000, 2, 63), grp(3000, 1, 64), grp(3000, 1, 65)]
     n_big = nmin + 9000 - sum(g.nconn for g in small)
@@ -372,7 +433,7 @@ def test_lane_path_vs_oracle(suite, version):
     nrec = sum(g.nconn * g.recs_per_conn for g in groups)
     ctype = rng.choice([21, 22, 23], nrec, p=[0.05, 0.05, 0.9])
     flags = np.where(rng.random(nrec) < 0.03, rng.integers(1, 4, nrec), 0)
-    wl = W.Workload("lane", groups, 72, rec_ctype=ctype, rec_flags=flags)
+    wl = W.Workload("many", groups, 72, rec_ctype=ctype, rec_flags=flags)
     wl.to_device()
     assert [n for _, _, n in wl.launches] == [wl.n_chains] and wl.n_chains > nmin
     wl.launch()

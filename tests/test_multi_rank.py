@@ -1,15 +1,17 @@
-"""N>1 path on CPU: two gloo ranks shard config-4-style connections exactly
-as bench.py does (tlslite_amd.shard), each seals its shard (with the CPU
-oracle standing in for the GPU, this is a sharding/aggregation test), and the
-gathered result must equal the single-process run; the max/sum reductions
-used for the bench line are exercised too."""
+"""N>1 path on CPU: two ranks shard config-4-style connections exactly as
+bench.py does (tlslite_amd.shard, its own TCP rendezvous -- no PyTorch), each
+seals its shard (with the CPU oracle standing in for the GPU, this is a
+sharding/aggregation test), and the gathered result must equal the
+single-process run; the max/sum reductions used for the bench line are
+exercised too."""
 import hashlib
 import os
 import socket
 
+import multiprocessing as mp
+
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 
 def _free_port():
@@ -46,7 +48,7 @@ def _worker(rank, world, port, q):
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from tlslite_amd import workloads as W
     from tlslite_amd.shard import ShardGroup, shard_indices
-    g = ShardGroup("gloo")
+    g = ShardGroup()
     wl = W.cfg4(nconn=6, recs_per_conn=3, pt_len=700, rank=rank, world=world)
     mine = shard_indices(6, rank, world)
     digests = _seal_shard(wl)
@@ -87,11 +89,15 @@ import hashlib, json, os, sys
 sys.path.insert(0, os.environ["TG_ROOT"])
 import numpy as np
 from tlslite_amd import workloads as W
-from tlslite_amd.device import Stream, set_device, synchronize
+from tlslite_amd.device import Stream, device_count, set_device, synchronize
 from tlslite_amd.recordlayer import SealPipeline, seal_dev
-from tlslite_amd.shard import ShardGroup, shard_indices
-g = ShardGroup("gloo")
-set_device(0)  # both ranks on the one GPU of the box: the per-device paths still run twice
+from tlslite_amd.shard import ShardGroup, device_for_rank, shard_indices
+g = ShardGroup()
+# one GPU per rank (LOCAL_RANK % devices): distinct devices on a multi-GPU node, both
+# ranks on the one GPU of a single-GPU box (the per-device paths then still run twice)
+dev = device_for_rank(g.local, device_count())
+set_device(dev)
+print("DEVICE %d %d" % (g.rank, dev), file=sys.stderr)
 wl = W.cfg4(nconn=64, recs_per_conn=4, pt_len=3000, rank=g.rank, world=g.world)
 wl.to_device()
 synchronize()
@@ -132,7 +138,7 @@ if g.rank == 0:
 
 @pytest.mark.gpu
 def test_two_rank_hip_sharding_matches_oracle(tmp_path):
-    """Two processes (RANK 0/1, gloo rendezvous, both on device 0) each seal
+    """Two processes (RANK 0/1, the shard rendezvous, device LOCAL_RANK % count) each seal
     their round-robin shard of 64 chained connections through libtlsgpu.so --
     batch 1 with tlsgpu_seal_dev and the library-owned workspace, batch 2
     through the seal pipeline with the states batch 1 left -- and the merged

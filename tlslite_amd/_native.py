@@ -17,7 +17,7 @@ FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
 OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH = 0, -1, -2, -3, -4, -5
 ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED, ALERT_SKIPPED = -20, -21, -22
 CHAIN_STOP_ON_ALERT = 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 CONN_STATE_BYTES = 2048
 
 
@@ -67,6 +67,7 @@ SIGNATURES = [
     ("tlsgpu_get_device", _i, [ctypes.POINTER(_i)]),
     ("tlsgpu_device_synchronize", _i, []),
     ("tlsgpu_device_arch", _i, [_i, ctypes.c_char_p, _sz]),
+    ("tlsgpu_device_cu_count", _i, [_i, ctypes.POINTER(_i)]),
     ("tlsgpu_malloc", _i, [ctypes.POINTER(_vp), _sz]),
     ("tlsgpu_free", _i, [_vp]),
     ("tlsgpu_host_alloc", _i, [ctypes.POINTER(_vp), _sz]),
@@ -93,7 +94,8 @@ SIGNATURES = [
     ("tlsgpu_conn_state_variant", _i, [_vp, ctypes.POINTER(_u32)]),
     ("tlsgpu_seal_wire_len", _i, [_vp, _u32, ctypes.POINTER(_u32)]),
     ("tlsgpu_seal_workspace_bytes", _sz, [_u32]),
-    ("tlsgpu_seal_lane_min_chains", _i, [ctypes.POINTER(_u32)]),
+    ("tlsgpu_release_workspaces", _i, []),
+    ("tlsgpu_seal_cipher_kernel", _i, [_u32, _u32, ctypes.c_char_p, _sz]),
     ("tlsgpu_seal_dev", _i, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
     ("tlsgpu_pipeline_create", _i, [ctypes.POINTER(_vp), _u32]),
     ("tlsgpu_pipeline_destroy", _i, [_vp]),

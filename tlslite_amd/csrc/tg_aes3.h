@@ -55,7 +55,8 @@ template <int CIPHER_ID, int MAC, bool SSL3>
 __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
                                                     const tlsgpu_record* __restrict__ recs,
                                                     ConnState* __restrict__ states, int32_t* __restrict__ wire_len,
-                                                    RecMeta* __restrict__ meta, uint32_t nrecords, uint32_t epoch) {
+                                                    RecMeta* __restrict__ meta, uint32_t nrecords, uint32_t epoch,
+                                                    uint64_t wire_cap) {
     const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
@@ -86,6 +87,8 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
                 wire_len[r] = 0;
             } else if (body > 0xffffu) {
                 wire_len[r] = TLSGPU_ETOOBIG;
+            } else if ((uint64_t)recs[r].wire_off + 5u + body > wire_cap) {
+                wire_len[r] = TLSGPU_EINVAL;  // the sealed record would end past the wire arena
             } else {
                 const uint32_t rb = n & (BS - 1);
                 m.status = 1;
@@ -117,10 +120,14 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_DES_ANDOR     3DES SP-box address by v_and_or_b32 instead of v_bitop3
 //   TG_AB_OPEN_QUAD     AES open decrypt on the quad layout (open_dec_kernel, round 1) instead of
 //                       one lane per block (open_aes_kernel)
-//   TG_AB_LANE_SEAL     AES seal with one lane per chain for many-chain batches (tg_lane.h), with
-//                       TG_AB_LS_WAVES / TG_AB_LS_MIN_PER_CU (its wave count and dispatch
-//                       threshold) and TG_AB_LS_NOLOAD / _NOSTORE / _NOMEM (timing only: bulk
-//                       plaintext loads / ciphertext stores / both left out)
+//   TG_AB_PAIR       cipher phase with 2 lanes per chain (cbc_pair_kernel) when a CU gets at least
+//                    C3_CHAINS chains; TG_AB_PAIR_WAVES / TG_AB_PAIR_WAVES_MANY its waves per CU
+#ifndef TG_AB_PAIR_WAVES
+#define TG_AB_PAIR_WAVES 8
+#endif
+#ifndef TG_AB_PAIR_WAVES_MANY
+#define TG_AB_PAIR_WAVES_MANY 16
+#endif
 #ifndef TG_AB_MAC_PRIO
 #define TG_AB_MAC_PRIO 0
 #endif
@@ -314,10 +321,10 @@ __global__ void __launch_bounds__(256, LB) mac_kernel(const tlsgpu_record* __res
                                                  const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
                                                  const ConnState* __restrict__ states, int32_t* __restrict__ wire_len,
                                                  const RecMeta* __restrict__ meta, uint8_t* __restrict__ tails,
-                                                 uint32_t epoch) {
+                                                 uint32_t epoch, uint32_t r0) {
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
-    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t r = r0 + blockIdx.x * blockDim.x + threadIdx.x;  // records [r0, nrecords)
     // no early exit before the bulk: the lanes of a quad exchange loaded data (DPP)
     RecMeta mt = {};
     bool act = r < nrecords;
@@ -506,7 +513,12 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
     // same addresses and write back the same state.  A full wave runs the dependent round
     // faster than a mostly masked one (cfg4 cipher phase 130 -> 115 cycles per round at 512
     // chains, the clock unchanged at 2.39 GHz).
-    if (local >= cpw && (threadIdx.x >> 6) == 0) local %= cpw;
+    // Mirroring is only sound when every quad runs exactly one chain (one generation, in
+    // lockstep with its mirror inside the wave): a mirror must never start a chain its
+    // original is not running at the same time, or the two would race on st->iv and the
+    // wire.  The launcher only picks this kernel form with cpw < C3_CHAINS chains per CU,
+    // i.e. grid * cpw >= nchains; the guard keeps it so for any other caller.
+    if (local >= cpw && (threadIdx.x >> 6) == 0 && (uint64_t)gridDim.x * cpw >= nchains) local %= cpw;
     if (local >= cpw) return;
     // the prefix kernel validated the state: any record it marked status 1 belongs to a matching state
     __builtin_amdgcn_s_setprio(TG_AB_CBC_PRIO);
@@ -553,6 +565,155 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
         }
     }
     if (any) st->iv[q] = iv;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// cbc_pair_kernel: the cipher phase with 2 lanes per chain (PairAes, tg_quad.h) for the
+// throughput regimes (a CU gets at least a workgroup's worth of chains).  Lane h holds
+// state columns 2h, 2h+1 and moves 8 bytes per block (one dwordx2 load and store).
+// Same stream of work per chain as cbc_kernel: explicit IV, full P blocks in groups of
+// 8 with the next group prefetched, the MAC kernel's tail slot.
+template <bool AL>
+__device__ __forceinline__ uint2 ld64t(const uint8_t* p) {
+    if constexpr (AL) return *(const uint2*)p;
+    return make_uint2(ld32t<false>(p), ld32t<false>(p + 4));
+}
+template <bool AL>
+__device__ __forceinline__ void st64t(uint8_t* p, uint32_t a, uint32_t b) {
+    if constexpr (AL) {
+        *(uint2*)p = make_uint2(a, b);
+    } else {
+        st32t<false>(p, a);
+        st32t<false>(p + 4, b);
+    }
+}
+
+// c = E(p ^ prev): (va, vb) is the chain's residue in, the ciphertext out
+template <int NR>
+__device__ __forceinline__ void pair_block(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
+                                           const uint32_t* kb, uint32_t& va, uint32_t& vb, uint32_t pa, uint32_t pb) {
+    uint32_t a = __builtin_amdgcn_bitop3_b32(pa, va, kw[0], 0x96);
+    uint32_t b = __builtin_amdgcn_bitop3_b32(pb, vb, kw[1], 0x96);
+    aes.encrypt_w<NR>(a, b, ka, kb);
+    va = a;
+    vb = b;
+}
+
+template <int NR, bool AL, bool CLAMP>
+__device__ __forceinline__ void pcbc_group8(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
+                                            const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
+                                            uint8_t* O, uint32_t b0, uint32_t last, uint2 f[8]) {
+    uint2 c[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) c[i] = f[i];
+    if constexpr (CLAMP) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t b = b0 + 8 + i;
+            f[i] = ld64t<AL>(P + 16 * (b < last ? b : last));
+        }
+    } else {
+        const uint8_t* Pn = P + 16 * (b0 + 8);
+#pragma unroll
+        for (int i = 0; i < 8; i++) f[i] = ld64t<AL>(Pn + 16 * i);
+    }
+    uint8_t* Ob = O + 16 * b0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        pair_block<NR>(aes, kw, ka, kb, va, vb, c[i].x, c[i].y);
+        st64t<AL>(Ob + 16 * i, va, vb);
+    }
+}
+
+template <int NR, bool AL>
+__device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
+                                          const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
+                                          uint8_t* O, uint32_t nb) {
+    if (nb == 0) return;
+    const uint32_t last = nb - 1;
+    uint2 f[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) f[i] = ld64t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
+    uint32_t b0 = 0;
+    if (nb >= 16) {  // first group peeled, as cbc_bulk
+        pcbc_group8<NR, AL, false>(aes, kw, ka, kb, va, vb, P, O, 0, last, f);
+        for (b0 = 8; b0 + 16 <= nb; b0 += 8) pcbc_group8<NR, AL, false>(aes, kw, ka, kb, va, vb, P, O, b0, last, f);
+    }
+    if (b0 + 8 <= nb) {
+        pcbc_group8<NR, AL, true>(aes, kw, ka, kb, va, vb, P, O, b0, last, f);
+        b0 += 8;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        if (b0 + i < nb) {
+            pair_block<NR>(aes, kw, ka, kb, va, vb, f[i].x, f[i].y);
+            st64t<AL>(O + 16 * (b0 + i), va, vb);
+        }
+    }
+}
+
+template <int NR, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES, 1)
+cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
+                uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
+                ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,
+                uint32_t cpw, uint32_t epoch) {
+    aes_lds_fill(nullptr, false);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t local = (threadIdx.x >> 6) * 32 + (lane >> 1);
+    const uint32_t h = lane & 1;
+    if (local >= cpw) return;  // both lanes of a pair leave together
+    __builtin_amdgcn_s_setprio(TG_AB_CBC_PRIO);
+    PairAes aes;
+    aes.init();
+    // persistent over chain generations (as cbc_kernel)
+    for (uint32_t cid = blockIdx.x * cpw + local; cid < nchains; cid += gridDim.x * cpw) {
+        const tlsgpu_chain ch = chains[cid];
+        ConnState* st = states + ch.state;
+        uint32_t kw[2], ka[NR + 1], kb[NR + 1];
+        PairAes::round_keys<NR>(st->ek, h, kw, ka, kb);
+        uint32_t va = st->iv[2 * h], vb = st->iv[2 * h + 1];
+        const uint32_t fa = st->fixed_iv[2 * h], fb = st->fixed_iv[2 * h + 1];
+        const uint32_t E = st->explicit_iv ? 16u : 0u;
+        bool any = false;
+        for (uint32_t j = 0; j < ch.count; j++) {
+            const uint32_t r = ch.first + j;
+            if (r >= nrecords) break;
+            const RecMeta mt = meta[r];
+            if (mt.epoch != epoch || mt.status != 1) continue;
+            any = true;
+            const tlsgpu_record R = recs[r];
+            const uint32_t n = R.pt_len;
+            const uint8_t* P = pt + R.pt_off + 8 * h;
+            uint8_t* B = wire + R.wire_off + 5;
+            const bool al = (((uintptr_t)(pt + R.pt_off) | (uintptr_t)B) & 7) == 0;
+            if (E) {  // E_K(fixedIVBlock ^ residue) (tlsrecordlayer.py:594-595)
+                pair_block<NR>(aes, kw, ka, kb, va, vb, fa, fb);
+                if (al) st64t<true>(B + 8 * h, va, vb);
+                else st64t<false>(B + 8 * h, va, vb);
+            }
+            uint8_t* O = B + E + 8 * h;
+            const uint32_t nb = n >> 4;
+            if (al) pcbc_bulk<NR, true>(aes, kw, ka, kb, va, vb, P, O, nb);
+            else pcbc_bulk<NR, false>(aes, kw, ka, kb, va, vb, P, O, nb);
+            // tail blocks from the MAC kernel's slot (8-byte aligned)
+            const uint32_t r16 = n & 15;
+            const uint8_t* slot = tails + (size_t)r * TAIL_SLOT + 8 * h;
+            uint8_t* Ot = B + E + (n - r16) + 8 * h;
+            const uint32_t T = mt.tail_len;
+            for (uint32_t off = 0; off < T; off += 16) {
+                const uint2 p = *(const uint2*)(slot + off);
+                pair_block<NR>(aes, kw, ka, kb, va, vb, p.x, p.y);
+                if (al) st64t<true>(Ot + off, va, vb);
+                else st64t<false>(Ot + off, va, vb);
+            }
+        }
+        if (any) {
+            st->iv[2 * h] = va;
+            st->iv[2 * h + 1] = vb;
+        }
     }
 }
 

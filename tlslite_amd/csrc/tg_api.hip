@@ -6,6 +6,7 @@
 #include <string.h>
 #include <stdio.h>
 #include <map>
+#include <set>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -93,6 +94,11 @@ int tlsgpu_device_arch(int ordinal, char* name, size_t cap) {
     hipDeviceProp_t p;
     TG_HIP(hipGetDeviceProperties(&p, ordinal));
     snprintf(name, cap, "%s", p.gcnArchName);
+    return 0;
+}
+int tlsgpu_device_cu_count(int ordinal, int* n) {
+    if (!n) return fail(TLSGPU_EINVAL, "null pointer");
+    TG_HIP(hipDeviceGetAttribute(n, hipDeviceAttributeMultiprocessorCount, ordinal));
     return 0;
 }
 
@@ -242,32 +248,60 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state* st, uint32_t pt_len, uint32_t*
 
 size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords) { return seal_workspace_bytes(nrecords); }
 
-int tlsgpu_seal_lane_min_chains(uint32_t* nchains) {
-    if (!nchains) return fail(TLSGPU_EINVAL, "null pointer");
-    *nchains = seal_lane_min_chains();
+int tlsgpu_seal_cipher_kernel(uint32_t variant, uint32_t nchains, char* name, size_t cap) {
+    if (!name || !cap) return fail(TLSGPU_EINVAL, "null name buffer");
+    const std::string k = seal_cipher_kernel(variant, nchains);
+    if (k.empty()) return fail(TLSGPU_EINVAL, "unsupported seal variant");
+    snprintf(name, cap, "%s", k.c_str());
+    return k.size() < cap ? 0 : fail(TLSGPU_EINVAL, "name buffer too small");
+}
+
+
+// library-owned workspace: one grow-only buffer per (kind, device, stream), so calls
+// on different streams never share one and calls on one stream are ordered by it;
+// tlsgpu_release_workspaces() frees them all (a caller that creates and destroys many
+// streams calls it, or the buffers live until the process ends)
+namespace {
+struct OwnKey {
+    int kind, dev;
+    hipStream_t s;
+    bool operator<(const OwnKey& o) const {
+        return kind != o.kind ? kind < o.kind : dev != o.dev ? dev < o.dev : s < o.s;
+    }
+};
+struct OwnBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+std::mutex own_mu;
+std::map<OwnKey, OwnBuf> own_bufs;
+}  // namespace
+
+int tlsgpu_release_workspaces(void) {
+    std::lock_guard<std::mutex> g(own_mu);
+    int cur = 0;
+    TG_HIP(hipGetDevice(&cur));
+    std::set<int> synced;
+    for (auto& kv : own_bufs) {
+        // the stream may be gone: wait for the whole device once before freeing its buffers
+        if (!synced.count(kv.first.dev)) {
+            TG_HIP(hipSetDevice(kv.first.dev));
+            TG_HIP(hipDeviceSynchronize());
+            synced.insert(kv.first.dev);
+        }
+        TG_HIP(hipSetDevice(kv.first.dev));
+        TG_HIP(hipFree(kv.second.p));
+    }
+    own_bufs.clear();
+    TG_HIP(hipSetDevice(cur));
     return 0;
 }
 
-// library-owned workspace: one grow-only buffer per (kind, device, stream), so calls
-// on different streams never share one and calls on one stream are ordered by it
 static int own_workspace(int kind, size_t need, hipStream_t stream, uint8_t** out) {
-    struct Key {
-        int kind, dev;
-        hipStream_t s;
-        bool operator<(const Key& o) const {
-            return kind != o.kind ? kind < o.kind : dev != o.dev ? dev < o.dev : s < o.s;
-        }
-    };
-    struct Buf {
-        void* p = nullptr;
-        size_t bytes = 0;
-    };
-    static std::mutex mu;
-    static std::map<Key, Buf> own;
     int dev = 0;
     TG_HIP(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> g(mu);
-    Buf& b = own[Key{kind, dev, stream}];
+    std::lock_guard<std::mutex> g(own_mu);
+    OwnBuf& b = own_bufs[OwnKey{kind, dev, stream}];
     if (b.bytes < need) {
         if (b.p) {
             TG_HIP(hipStreamSynchronize(stream));  // earlier calls on this stream may still read it
@@ -402,9 +436,7 @@ namespace {
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
-    // zero: clear a fresh allocation (the wire arena: its copy ranges include the alignment
-    // gaps between records, which must not carry stale device memory to the host)
-    hipError_t ensure(size_t need, bool zero = false) {
+    hipError_t ensure(size_t need) {
         if (bytes >= need && p) return hipSuccess;
         if (p) {
             hipError_t e = hipFree(p);
@@ -414,7 +446,6 @@ struct DevBuf {
         bytes = 0;
         hipError_t e = hipMalloc(&p, need ? need : 1);
         if (e == hipSuccess) bytes = need;
-        if (e == hipSuccess && zero) e = hipMemset(p, 0, need ? need : 1);
         return e;
     }
     void release() {
@@ -479,6 +510,7 @@ void stage_copy(void* dst, const void* src, size_t n) {
 }
 struct SubBatch {
     uint32_t c0, c1;  // chains [c0, c1)
+    uint32_t r0, r1;  // records its chains use: [r0, r1)
     size_t p0, p1;    // plaintext bytes copied H2D
     size_t w0, w1;    // wire bytes copied D2H
 };
@@ -564,6 +596,25 @@ int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p) {
     return 0;
 }
 
+// Largest record a seal of this variant can write for pt_len plaintext bytes: the 5-byte
+// header and the body [explicit IV] | P | MAC | padding (tlsrecordlayer.py:594-606), taking
+// the explicit IV (TLS >= 1.1, a state field the host does not see) when it makes the body
+// longer.  0 for an unknown variant.
+static uint64_t sealed_max_bytes(uint32_t variant, uint64_t n) {
+    const uint32_t c = variant & 0xff, m = (variant >> 8) & 0xff;
+    const uint64_t dl = m == TLSGPU_MAC_SHA1 ? 20 : m == TLSGPU_MAC_SHA256 ? 32 : m == TLSGPU_MAC_MD5 ? 16 : 0;
+    if (!dl) return 0;
+    if (c == TLSGPU_CIPHER_RC4) return 5 + n + dl;
+    const uint64_t bs = c == TLSGPU_CIPHER_3DES ? 8 : (c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256) ? 16 : 0;
+    if (!bs) return 0;
+    uint64_t body = 0;
+    for (uint64_t e : {(uint64_t)0, bs}) {
+        const uint64_t cur = e + n + dl, b = cur + (bs - (cur & (bs - 1)));
+        body = b > body ? b : body;
+    }
+    return 5 + body;
+}
+
 int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains, uint32_t nchains,
                               const tlsgpu_record* records, uint32_t nrecords, const uint8_t* pt_host,
                               size_t pt_bytes, uint8_t* wire_host, size_t wire_bytes, tlsgpu_conn_state* states,
@@ -572,23 +623,36 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
     if (nchains == 0) return 0;
     if (!chains || !records || !pt_host || !wire_host || !states || !wire_len_host)
         return fail(TLSGPU_EINVAL, "null pointer");
+    if (!sealed_max_bytes(variant, 0)) return fail(TLSGPU_EINVAL, "unsupported seal variant");
+    const bool need_ws = seal_needs_workspace(variant);
     // sub-batches of consecutive chains, about p->chunk plaintext bytes each
     std::vector<SubBatch> sub;
     std::vector<size_t> pmin, wmin, pend, wend;  // per sub-batch extremes over its records
     {
-        SubBatch cur = {0, 0, 0, 0, 0, 0};
+        SubBatch cur = {0, 0, UINT32_MAX, 0, 0, 0, 0, 0};
         size_t acc = 0, lo_p = SIZE_MAX, lo_w = SIZE_MAX, hi_p = 0, hi_w = 0;
         for (uint32_t c = 0; c < nchains; c++) {
             const tlsgpu_chain& ch = chains[c];
             if ((uint64_t)ch.first + ch.count > nrecords) return fail(TLSGPU_EINVAL, "chain outside the records");
+            if (ch.count) {
+                cur.r0 = ch.first < cur.r0 ? ch.first : cur.r0;
+                cur.r1 = ch.first + ch.count > cur.r1 ? ch.first + ch.count : cur.r1;
+            }
             for (uint32_t k = 0; k < ch.count; k++) {
                 const tlsgpu_record& R = records[ch.first + k];
-                if (R.pt_off + R.pt_len > pt_bytes || R.wire_off + 5 + (uint64_t)R.pt_len > wire_bytes)
+                // A record's wire slot must hold its sealed form, not just 5 + P: the kernels
+                // write the tail, MAC and padding past it.  RC4's size is known here; a CBC
+                // record's depends on the state's explicit-IV flag (device-resident), so the
+                // prefix kernel checks its exact end against wire_bytes (SealBounds) and this
+                // check only needs the header and the plaintext length in range.
+                const uint64_t wext = (uint64_t)R.wire_off + (need_ws ? 5 + (uint64_t)R.pt_len
+                                                                      : sealed_max_bytes(variant, R.pt_len));
+                if ((uint64_t)R.pt_off + R.pt_len > pt_bytes || wext > wire_bytes)
                     return fail(TLSGPU_EINVAL, "record outside the host arenas");
                 lo_p = R.pt_off < lo_p ? R.pt_off : lo_p;
                 lo_w = R.wire_off < lo_w ? R.wire_off : lo_w;
                 hi_p = R.pt_off + R.pt_len > hi_p ? R.pt_off + R.pt_len : hi_p;
-                hi_w = R.wire_off + 5 + R.pt_len > hi_w ? R.wire_off + 5 + R.pt_len : hi_w;
+                hi_w = wext > hi_w ? wext : hi_w;
                 acc += R.pt_len;
             }
             cur.c1 = c + 1;
@@ -599,6 +663,8 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
                 pend.push_back(hi_p);
                 wend.push_back(hi_w);
                 cur.c0 = c + 1;
+                cur.r0 = UINT32_MAX;
+                cur.r1 = 0;
                 acc = 0;
                 lo_p = lo_w = SIZE_MAX;
                 hi_p = hi_w = 0;
@@ -611,7 +677,7 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
             if (pend[i] > pmin[i + 1] || wend[i] > wmin[i + 1] || pmin[i + 1] < pmin[i] || wmin[i + 1] < wmin[i])
                 mono = false;
         if (!mono) {
-            sub.assign(1, SubBatch{0, nchains, 0, 0, 0, 0});
+            sub.assign(1, SubBatch{0, nchains, 0, nrecords, 0, 0, 0, 0});
             pmin.assign(1, 0);
             wmin.assign(1, 0);
         }
@@ -630,11 +696,13 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
         max_w = b.w1 - b.w0 > max_w ? b.w1 - b.w0 : max_w;
     }
     TG_HIP(p->pt.ensure(pt_bytes));
-    TG_HIP(p->wire.ensure(wire_bytes, true));
+    TG_HIP(p->wire.ensure(wire_bytes));
+    // the D2H ranges include the gaps between records: they come back as zeros, never as
+    // bytes an earlier batch left in the device arena (h2d stream: before every seal kernel)
+    TG_HIP(hipMemsetAsync(p->wire.p, 0, wire_bytes, p->h2d));
     TG_HIP(p->recs.ensure((size_t)nrecords * sizeof(tlsgpu_record)));
     TG_HIP(p->chains.ensure((size_t)nchains * sizeof(tlsgpu_chain)));
     TG_HIP(p->len.ensure((size_t)nrecords * 4));
-    const bool need_ws = seal_needs_workspace(variant);
     for (int i = 0; i < D; i++) {
         if (need_ws) TG_HIP(p->ws[i].ensure(seal_workspace_bytes(nrecords)));
         if (!pt_direct) TG_HIP(p->pt_stage[i].ensure(max_p));
@@ -674,9 +742,13 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
         bool known = false;
         hipError_t e;
         if (need_ws) {
+            SealBounds sb;
+            sb.rec_lo = b.r0 < b.r1 ? b.r0 : 0;
+            sb.rec_hi = b.r0 < b.r1 ? b.r1 : 0;
+            sb.wire_cap = wire_bytes;
             e = launch_seal_phases(variant, d_chains + b.c0, b.c1 - b.c0, d_recs, nrecords, p->pt.u8(), p->wire.u8(),
                                    S(states), static_cast<int32_t*>(p->len.p), p->ws[t].u8(), next_epoch(), p->mac,
-                                   p->mac_done[t], p->cbc, nullptr, nullptr, &known);
+                                   p->mac_done[t], p->cbc, nullptr, nullptr, &known, sb);
         } else {  // single-kernel variants (RC4) on the cipher stream
             TG_HIP(hipStreamWaitEvent(p->cbc, p->in_done[t], 0));
             e = launch_seal(variant, d_chains + b.c0, b.c1 - b.c0, d_recs, nrecords, p->pt.u8(), p->wire.u8(),

@@ -17,11 +17,9 @@
 #include "tg_quad.h"
 #include "tg_aes3.h"
 #include "tg_open3.h"
-#ifdef TG_AB_LANE_SEAL
-#include "tg_lane.h"
-#endif
 #include "tg_derive.h"
 #include "tg_launch.h"
+#include <string>
 
 namespace tg {
 
@@ -359,21 +357,27 @@ static bool many_chains(uint32_t nchains) {
 template <int NR, int MAC, bool SSL3>
 static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
-                                   int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s) {
+                                   int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s,
+                                   const SealBounds& sb) {
     constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
     constexpr int BS = NR == 0 ? 8 : 16;
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
-    hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(RecMeta), s);
+    // the records this launch's chains use (a host-pipeline sub-batch: its own window)
+    const uint32_t r1 = sb.rec_hi < nrecords ? sb.rec_hi : nrecords;
+    const uint32_t r0 = sb.rec_lo < r1 ? sb.rec_lo : r1;
+    if (r1 == r0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(meta + r0, 0, (size_t)(r1 - r0) * sizeof(RecMeta), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((prefix_kernel<CID, MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains,
-                       recs, states, wire_len, meta, nrecords, epoch);
+                       recs, states, wire_len, meta, nrecords, epoch, sb.wire_cap);
+    const dim3 grid((r1 - r0 + 255) / 256);
     if (NR != 0 && many_chains(nchains))
-        hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS, MAC_LB_MANY, MAC_PF_MANY>), dim3((nrecords + 255) / 256), dim3(256),
-                           0, s, recs, nrecords, pt, wire, states, wire_len, meta, tails, epoch);
+        hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS, MAC_LB_MANY, MAC_PF_MANY>), grid, dim3(256), 0, s, recs, r1, pt,
+                           wire, states, wire_len, meta, tails, epoch, r0);
     else
-        hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS>), dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords,
-                           pt, wire, states, wire_len, meta, tails, epoch);
+        hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS>), grid, dim3(256), 0, s, recs, r1, pt, wire, states, wire_len,
+                           meta, tails, epoch, r0);
     return hipGetLastError();
 }
 
@@ -395,6 +399,23 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         return hipGetLastError();
     } else {
         const bool many = many_chains(nchains);
+#ifdef TG_AB_PAIR
+        if (nchains >= (uint32_t)C3_CHAINS * ncu) {
+            // throughput regimes: 2 lanes per chain (cbc_pair_kernel)
+            constexpr uint32_t W1 = TG_AB_PAIR_WAVES, WM = TG_AB_PAIR_WAVES_MANY;
+            const uint32_t pwg = many ? 32u * WM : 32u * W1;
+            uint32_t cpw = (nchains + ncu - 1) / ncu;
+            cpw = cpw > pwg ? pwg : cpw;
+            auto kern = many ? cbc_pair_kernel<NR, WM> : cbc_pair_kernel<NR, W1>;
+            hipError_t e = set_lds(kern, AES_LDS_BYTES);
+            if (e != hipSuccess) return e;
+            uint32_t grid = (nchains + cpw - 1) / cpw;
+            grid = grid > ncu ? ncu : grid;
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (many ? WM : W1)), AES_LDS_BYTES, s, chains, nchains, recs,
+                               nrecords, pt, wire, states, meta, tails, cpw, epoch);
+            return hipGetLastError();
+        }
+#endif
         const uint32_t wg_chains = many ? 16u * C3_WAVES_MANY : (uint32_t)C3_CHAINS;
         uint32_t cpw = (nchains + ncu - 1) / ncu;
         cpw = cpw < 1 ? 1 : (cpw > wg_chains ? wg_chains : cpw);
@@ -412,41 +433,28 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
     }
 }
 
-// The lane-per-chain AES seal (tg_lane.h) is an A/B build (TG_AB_LANE_SEAL): on cfg3 it
-// measured slower than the split path (best 2.84 vs 2.73 ms per step),
-// so the product library never selects it and reports "never" (UINT32_MAX).
-#ifdef TG_AB_LANE_SEAL
-#ifndef TG_AB_LS_MIN_PER_CU
-#define TG_AB_LS_MIN_PER_CU LS_THREADS
-#endif
-uint32_t seal_lane_min_chains() { return (uint32_t)TG_AB_LS_MIN_PER_CU * cu_count(); }
-#else
-uint32_t seal_lane_min_chains() { return 0xffffffffu; }
-#endif
-static bool use_lane_seal(uint32_t nchains) { return nchains >= seal_lane_min_chains(); }
-
-#ifdef TG_AB_LANE_SEAL
-template <int NR, int MAC, bool SSL3>
-static hipError_t launch_lane_seal(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
-                                   uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
-                                   int32_t* wire_len, hipStream_t s) {
-    auto kern = lseal_kernel<NR, MAC, SSL3>;
-    hipError_t e = set_lds(kern, AES_LDS_BYTES);
-    if (e != hipSuccess) return e;
+// The cipher-phase kernel launch_cbc_phase / launch_seal picks for a call of nchains
+// chains on the current device, as rocprofv3 names it (bench.py's dominant kernel).
+std::string seal_cipher_kernel(uint32_t variant, uint32_t nchains) {
+    const uint32_t c = variant & 0xff;
+    if (c == TLSGPU_CIPHER_RC4) return "rc4_seal_kernel";
+    if (c == TLSGPU_CIPHER_3DES) return "tdes4_kernel";
+    if (c != TLSGPU_CIPHER_AES128 && c != TLSGPU_CIPHER_AES256) return "";
+    const int nr = c == TLSGPU_CIPHER_AES128 ? 10 : 14;
     const uint32_t ncu = cu_count();
-    uint32_t grid = (nchains + LS_THREADS - 1) / LS_THREADS;
-    grid = grid > ncu ? ncu : grid;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(LS_THREADS), AES_LDS_BYTES, s, chains, nchains, recs, nrecords, pt, wire,
-                       states, wire_len);
-    return hipGetLastError();
-}
-#else
-template <int NR, int MAC, bool SSL3>
-static hipError_t launch_lane_seal(const tlsgpu_chain*, uint32_t, const tlsgpu_record*, uint32_t, const uint8_t*,
-                                   uint8_t*, ConnState*, int32_t*, hipStream_t) {
-    return hipErrorInvalidDeviceFunction;  // unreachable: use_lane_seal() is false in this build
-}
+    const bool many = many_chains(nchains);
+    char b[64];
+#ifdef TG_AB_PAIR
+    if (nchains >= (uint32_t)C3_CHAINS * ncu) {
+        snprintf(b, sizeof b, "cbc_pair_kernel<%d, %d>", nr, many ? TG_AB_PAIR_WAVES_MANY : TG_AB_PAIR_WAVES);
+        return b;
+    }
 #endif
+    const uint32_t cpw = (nchains + ncu - 1) / ncu;
+    if (many) snprintf(b, sizeof b, "cbc_kernel<%d, false, %d>", nr, C3_WAVES_MANY);
+    else snprintf(b, sizeof b, "cbc_kernel<%d, %s>", nr, cpw < (uint32_t)C3_CHAINS ? "true" : "false");
+    return b;
+}
 
 // The (cipher, MAC, SSL3) variants of the split seal path (AES and 3DES suites)
 #define TG_SPLIT_VARIANTS(X)                             \
@@ -464,29 +472,13 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
                               const tlsgpu_record* recs, uint32_t nrecords, const uint8_t* pt, uint8_t* wire,
                               ConnState* states, int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s1,
                               hipEvent_t mac_done, hipStream_t s2, hipEvent_t cbc_start, hipEvent_t cbc_stop,
-                              bool* known) {
+                              bool* known, const SealBounds& sb) {
     *known = true;
     hipError_t e = hipSuccess;
 #define TG_PH(CID, NR, MAC_ID, SSL3)                                                                            \
-    if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3) && NR != 0 && use_lane_seal(nchains)) {                     \
-        /* one kernel after all earlier work of both streams; later work of both after it */                     \
-        if (s2 != s1) {                                                                                          \
-            if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                      \
-            if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                               \
-        }                                                                                                        \
-        if (cbc_start && (e = hipEventRecord(cbc_start, s2)) != hipSuccess) return e;                           \
-        e = launch_lane_seal<NR == 0 ? 10 : NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states,  \
-                                                             wire_len, s2);                                      \
-        if (e == hipSuccess && cbc_stop) e = hipEventRecord(cbc_stop, s2);                                       \
-        if (e == hipSuccess && s2 != s1) {                                                                       \
-            if ((e = hipEventRecord(mac_done, s2)) != hipSuccess) return e;                                      \
-            e = hipStreamWaitEvent(s1, mac_done, 0);                                                             \
-        }                                                                                                        \
-        return e;                                                                                                \
-    }                                                                                                            \
     if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3)) {                                                          \
         e = launch_mac_phase<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,   \
-                                               epoch, s1);                                                       \
+                                               epoch, s1, sb);                                                   \
         if (e != hipSuccess) return e;                                                                           \
         if (s2 != s1) {                                                                                          \
             if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                      \

@@ -129,6 +129,60 @@ struct QuadAes {
     }
 };
 
+// The AES round for 2 lanes per block ("pair"): lane h holds state columns a = 2h and
+// b = 2h+1.  Column j of the next state = T0[b0(s_j)] ^ T1[b1(s_j+1)] ^ T2[b2(s_j+2)] ^
+// T3[b3(s_j+3)] ^ k_j (rijndael.py:304-310): of the 16 lookups the lane does the 8 that
+// read its own two columns; 4 of them belong to its own output columns, the other 4
+// (with the partner's key columns folded in) are sent to the partner -- one DPP swap
+// per column.  Per 32 blocks (a wave) a round is 8 lookups + 12 VALU (6 v_perm, 2 DPP)
+// against 16 lookups + 32 VALU (12 v_perm, 12 DPP) for two quad waves: 20 % fewer VALU
+// cycles per block-round, so the MAC phase running beside the cipher phase gets more issue
+// slots (tools/aes_layout_microbench.hip "pair1").
+struct PairAes : QuadAes {
+    // quad_perm [1,0,3,2]: the partner lane (bound_ctrl: no "old" register)
+    static __device__ __forceinline__ uint32_t swap(uint32_t v) { return quad_dpp<0xB1>(v); }
+    __device__ __forceinline__ void round(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
+        const uint32_t a2 = look<2, 2>(a), b3 = look<3, 3>(b), a1 = look<1, 1>(a), b2 = look<2, 2>(b);
+        const uint32_t a0 = look<0, 0>(a), b1 = look<1, 1>(b), b0 = look<0, 0>(b), a3 = look<3, 3>(a);
+        const uint32_t sa = __builtin_amdgcn_bitop3_b32(a2, b3, ka, 0x96);  // partner's column 2h+2
+        const uint32_t sb = __builtin_amdgcn_bitop3_b32(a1, b2, kb, 0x96);  // partner's column 2h+3
+        a = (a0 ^ b1) ^ swap(sa);
+        b = (b0 ^ a3) ^ swap(sb);
+    }
+    // final round: S-box byte B of s sits at byte B of table (B+2)&3
+    __device__ __forceinline__ void last(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
+        const uint32_t ta0 = look<2, 0>(a), tb1 = look<3, 1>(b), ta2 = look<0, 2>(a), tb3 = look<1, 3>(b);
+        const uint32_t tb0 = look<2, 0>(b), ta3 = look<1, 3>(a), ta1 = look<3, 1>(a), tb2 = look<0, 2>(b);
+        const uint32_t oa = perm(tb1, ta0, 0x0c0c0500u);
+        const uint32_t sa = perm(tb3, ta2, 0x07020c0cu) ^ ka;
+        const uint32_t ob = perm(ta3, tb0, 0x070c0c00u);
+        const uint32_t sb = perm(tb2, ta1, 0x0c06010cu) ^ kb;
+        a = oa ^ swap(sa);
+        b = ob ^ swap(sb);
+    }
+    // round keys: kw[0..1] = whitening columns 2h, 2h+1; ka/kb[r >= 1] = the partner's
+    // columns 2(1-h), 2(1-h)+1 of round key r (folded into the terms sent to it)
+    template <int NR>
+    static __device__ __forceinline__ void round_keys(const uint32_t* ek, uint32_t h, uint32_t* kw, uint32_t* ka,
+                                                      uint32_t* kb) {
+        kw[0] = ek[2 * h];
+        kw[1] = ek[2 * h + 1];
+        const uint32_t pa = 2 * (1 - h);
+#pragma unroll
+        for (int r = 1; r <= NR; r++) {
+            ka[r] = ek[4 * r + pa];
+            kb[r] = ek[4 * r + pa + 1];
+        }
+    }
+    // one block whose two columns are already whitened
+    template <int NR>
+    __device__ __forceinline__ void encrypt_w(uint32_t& a, uint32_t& b, const uint32_t* ka, const uint32_t* kb) const {
+#pragma unroll
+        for (int r = 1; r < NR; r++) round(a, b, ka[r], kb[r]);
+        last(a, b, ka[NR], kb[NR]);
+    }
+};
+
 __device__ __forceinline__ uint32_t ld32(const uint8_t* p, bool al) {
     if (al) return *(const uint32_t*)p;
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);

@@ -22,6 +22,19 @@ def synchronize():
     N.call("tlsgpu_device_synchronize")
 
 
+def current_device():
+    d = ctypes.c_int(0)
+    N.call("tlsgpu_get_device", ctypes.byref(d))
+    return d.value
+
+
+def cu_count(ordinal=None):
+    """Compute units of `ordinal` (default: the current device)."""
+    n = ctypes.c_int(0)
+    N.call("tlsgpu_device_cu_count", current_device() if ordinal is None else ordinal, ctypes.byref(n))
+    return n.value
+
+
 def arch(ordinal=0):
     buf = ctypes.create_string_buffer(64)
     N.call("tlsgpu_device_arch", ordinal, buf, 64)

@@ -114,13 +114,13 @@ def seal_workspace_bytes(nrecords):
     return int(N.lib.tlsgpu_seal_workspace_bytes(int(nrecords)))
 
 
-def seal_lane_min_chains():
-    """Chains per AES seal call from which the current device seals one lane per chain
-    (MAC and CBC of a record in one lane, tg_lane.h) instead of the split MAC / quad-CBC
-    path.  Same bytes either way."""
-    n = ctypes.c_uint32()
-    N.call("tlsgpu_seal_lane_min_chains", ctypes.byref(n))
-    return int(n.value)
+def seal_cipher_kernel(variant, nchains):
+    """The cipher-phase kernel (rocprofv3 name stem) a seal call of `nchains` chains of
+    `variant` runs on the current device: the library picks the layout from the chains
+    per CU (tlsgpu_seal_cipher_kernel)."""
+    buf = ctypes.create_string_buffer(96)
+    N.call("tlsgpu_seal_cipher_kernel", int(variant), int(nchains), buf, len(buf))
+    return buf.value.decode()
 
 
 def seal_dev(chains, nchains, records, nrecords, pt, wire, states, wire_len, variant, workspace=None, stream=None):

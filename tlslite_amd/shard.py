@@ -1,9 +1,18 @@
 """Connection sharding across GPUs: one process per GPU,
 connections dealt round-robin (`conn_id % world == rank`), no collective on
-the data path.  torch.distributed (gloo, CPU tensors) is used only for the
-start/stop barriers and the max-over-ranks / sum-over-ranks of the timing
-numbers -- plumbing, not the product."""
+the data path (a connection's records are serial: tlsrecordlayer.py:27-37,
+python_aes.py:44, so the connection is the shard unit).
+
+The ranks only meet for the bench's start/stop barriers, the max-over-ranks /
+sum-over-ranks of its timing numbers and a gather of check digests.  That is
+done by a small TCP rendezvous of our own (no PyTorch, no RCCL): rank 0 serves
+`MASTER_ADDR:(MASTER_PORT + 1)` -- `torch.distributed.run` keeps its own store on
+MASTER_PORT itself -- (or `TLSGPU_RDZV_PORT`), every other rank connects, and
+each collective is an all-gather of byte strings through rank 0."""
 import os
+import socket
+import struct
+import time
 
 import numpy as np
 
@@ -14,56 +23,116 @@ def shard_indices(n, rank, world):
     return np.arange(rank, n, world, dtype=np.int64)
 
 
+def device_for_rank(local_rank, device_count):
+    """The GPU a rank drives: one process per GPU (`local_rank % count`), so on a
+    node with fewer GPUs than ranks the ranks share devices round-robin."""
+    return int(local_rank) % max(int(device_count), 1)
+
+
+def _send(sock, b):
+    sock.sendall(struct.pack("<Q", len(b)) + b)
+
+
+def _recv_exact(sock, n):
+    buf = bytearray()
+    while len(buf) < n:
+        chunk = sock.recv(n - len(buf))
+        if not chunk:
+            raise ConnectionError("rendezvous peer closed the connection")
+        buf += chunk
+    return bytes(buf)
+
+
+def _recv(sock):
+    (n,) = struct.unpack("<Q", _recv_exact(sock, 8))
+    return _recv_exact(sock, n)
+
+
 class ShardGroup:
-    def __init__(self, backend="gloo"):
+    """RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT from the
+    environment (as torch.distributed.run sets them); world size 1 needs none."""
+
+    def __init__(self, timeout=120.0):
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local = int(os.environ.get("LOCAL_RANK", str(self.rank)))
-        self.dist = None
-        if self.world > 1:
-            import sys
-            import torch.distributed as dist
-            if not dist.is_initialized():
-                # gloo prints connection banners on fd 1; keep stdout for the
-                # bench's single JSON line
-                sys.stdout.flush()
-                saved = os.dup(1)
-                os.dup2(2, 1)
+        self._peers = []   # rank 0: sockets of ranks 1..world-1 in rank order
+        self._sock = None  # rank > 0: socket to rank 0
+        if self.world <= 1:
+            return
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ.get("TLSGPU_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
+        deadline = time.monotonic() + timeout
+        if self.rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((addr, port))
+            srv.listen(self.world)
+            srv.settimeout(timeout)
+            by_rank = {}
+            while len(by_rank) < self.world - 1:
+                c, _ = srv.accept()
+                c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                c.settimeout(None)
+                (r,) = struct.unpack("<I", _recv_exact(c, 4))
+                if r in by_rank or not 0 < r < self.world:
+                    raise RuntimeError("rendezvous: unexpected rank %d" % r)
+                by_rank[r] = c
+            srv.close()
+            self._peers = [by_rank[r] for r in range(1, self.world)]
+        else:
+            while True:
                 try:
-                    dist.init_process_group(backend)
-                finally:
-                    sys.stdout.flush()
-                    os.dup2(saved, 1)
-                    os.close(saved)
-            self.dist = dist
+                    s = socket.create_connection((addr, port), timeout=5.0)
+                    break
+                except OSError:
+                    if time.monotonic() > deadline:
+                        raise
+                    time.sleep(0.05)
+            s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            s.settimeout(None)
+            s.sendall(struct.pack("<I", self.rank))
+            self._sock = s
+
+    def all_gather(self, b):
+        """Every rank's byte string, in rank order, on every rank."""
+        b = bytes(b)
+        if self.world <= 1:
+            return [b]
+        if self.rank == 0:
+            parts = [b] + [_recv(c) for c in self._peers]
+            blob = struct.pack("<I", len(parts)) + b"".join(struct.pack("<Q", len(p)) + p for p in parts)
+            for c in self._peers:
+                _send(c, blob)
+            return parts
+        _send(self._sock, b)
+        blob = _recv(self._sock)
+        (n,) = struct.unpack_from("<I", blob, 0)
+        out, off = [], 4
+        for _ in range(n):
+            (L,) = struct.unpack_from("<Q", blob, off)
+            out.append(blob[off + 8:off + 8 + L])
+            off += 8 + L
+        return out
 
     def barrier(self):
-        if self.dist:
-            self.dist.barrier()
-
-    def _reduce(self, x, op):
-        if not self.dist:
-            return float(x)
-        import torch
-        t = torch.tensor([float(x)], dtype=torch.float64)
-        self.dist.all_reduce(t, op=op)
-        return float(t.item())
+        self.all_gather(b"")
 
     def max(self, x):
-        return self._reduce(x, self.dist.ReduceOp.MAX if self.dist else None)
+        return max(struct.unpack("<d", p)[0] for p in self.all_gather(struct.pack("<d", float(x))))
 
     def sum(self, x):
-        return self._reduce(x, self.dist.ReduceOp.SUM if self.dist else None)
+        return float(sum(struct.unpack("<d", p)[0] for p in self.all_gather(struct.pack("<d", float(x)))))
 
     def gather_bytes(self, b):
         """All ranks' byte strings (rank order); for checks only."""
-        if not self.dist:
-            return [bytes(b)]
-        out = [None] * self.world
-        self.dist.all_gather_object(out, bytes(b))
-        return out
+        return self.all_gather(b)
 
     def close(self):
-        if self.dist:
-            self.dist.destroy_process_group()
-            self.dist = None
+        if self.world > 1 and (self._peers or self._sock):
+            self.barrier()
+        for c in self._peers:
+            c.close()
+        if self._sock:
+            self._sock.close()
+        self._peers, self._sock = [], None

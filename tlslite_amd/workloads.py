@@ -175,6 +175,7 @@ class Workload:
         self.d_states.upload(st)
         # one chain array per variant
         self.launches = []
+        self.launch_alg_bytes = []
         var_of_group = [ConnectionState.for_suite(
             g.suite, g.version, bytes(g.keys[0]), bytes(g.ivs[0]) if g.ivs is not None else b"",
             bytes(g.mac_keys[0]), bytes(g.fixed_ivs[0]) if g.fixed_ivs is not None else None).variant
@@ -187,6 +188,10 @@ class Workload:
             d = DeviceBuffer(ctypes.sizeof(ch))
             d.upload(np.frombuffer(ch, dtype=np.uint8))
             self.launches.append((var, d, len(idx)))
+            recs = np.concatenate([np.arange(int(self.chain_first[c]), int(self.chain_first[c] + self.chain_count[c]))
+                                   for c in idx]) if idx else np.zeros(0, dtype=np.int64)
+            # algorithmic bytes of this launch (P read + 5+C written)
+            self.launch_alg_bytes.append(int(self.pt_len[recs].astype(np.int64).sum() + self.wire_len[recs].sum()))
         if fill:
             for off, n, start in self.fill_plan():
                 fill_pattern(self.d_pt, n, self.seed, start, off, stream)
@@ -268,12 +273,8 @@ class Workload:
         var, _, nch = self.launches[0]
         c, m = var & 0xff, (var >> 8) & 0xff
         if c in (N.CIPHER_AES128, N.CIPHER_AES256) and m in (N.MAC_SHA1, N.MAC_SHA256):
-            from .recordlayer import seal_lane_min_chains
-            nr = 10 if c == N.CIPHER_AES128 else 14
-            # many chains: one lane per chain, MAC + CBC in one kernel (tg_lane.h)
-            if nch >= seal_lane_min_chains():
-                return "lseal_kernel<%d, %d, %s>" % (nr, m, "true" if (var >> 16) & 1 else "false")
-            return "cbc_kernel<%d>" % nr
+            from .recordlayer import seal_cipher_kernel
+            return seal_cipher_kernel(var, nch)  # the layout the library picks for this many chains
         if c == N.CIPHER_3DES:
             # split path: bench.py's events bracket the whole 3DES seal call (prefix + MAC +
             # tdes4_kernel), which tdes4_kernel dominates

@@ -45,6 +45,17 @@ __device__ __forceinline__ uint32_t op(uint32_t a, uint32_t b, uint32_t c) {
     if constexpr (KIND == 31) asm volatile("v_lshlrev_b32_e32 %0, %1, %2" : "=v"(r) : "v"(c), "v"(a));
     if constexpr (KIND == 32) asm volatile("v_xor_b32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(r) : "v"(a), "v"(b));
     if constexpr (KIND == 33) asm volatile("v_and_b32_e32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    // SDWA (VOP1/VOP2 with byte selects): a T-table address built in one op -- byte b of the
+    // state word into bits 8..15 of the address register, its other bits (lane copy, table
+    // select) preserved from the previous round
+    if constexpr (KIND == 34) { r = a; asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(r) : "v"(b)); }
+    if constexpr (KIND == 35) asm volatile("v_lshlrev_b32_sdwa %0, 8, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(a));
+    if constexpr (KIND == 36) asm volatile("v_or_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(a), "v"(b));
+    if constexpr (KIND == 37) asm volatile("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    if constexpr (KIND == 38) asm volatile("v_alignbit_b32 %0, %1, %1, 27" : "=v"(r) : "v"(a));
+    if constexpr (KIND == 39) asm volatile("v_add_u32_e32 %0, 0x5a827999, %1" : "=v"(r) : "v"(a));
+    if constexpr (KIND == 40) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(r) : "v"(a));
+    if constexpr (KIND == 41) asm volatile("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     if constexpr (KIND >= 10) return r;
     return 0;
 }
@@ -63,7 +74,7 @@ __global__ void __launch_bounds__(1024) rate_kernel(uint32_t* out, uint64_t* cyc
         for (int r = 0; r < 8; r++)
 #pragma unroll
             for (int i = 0; i < 8; i++)
-                x[i] = op<KIND>(x[i], x[i ^ 4], (KIND == 3 || KIND == 13 || KIND == 14 || (KIND >= 18 && KIND != 31)) ? x[(i + 2) & 7] : KIND == 31 ? (c & 7) : c);
+                x[i] = op<KIND>(x[i], x[i ^ 4], (KIND == 3 || KIND == 13 || KIND == 14 || (KIND >= 18 && KIND != 31 && KIND < 34) || KIND == 37) ? x[(i + 2) & 7] : KIND == 31 ? (c & 7) : c);
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     uint32_t s = 0;
@@ -108,7 +119,7 @@ int main() {
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const int iters = 4096;
-    for (int w : {4}) {
+    for (int w : {1, 4}) {
         run<26>("v_lshrrev_b32 const", cus, w, iters);
         run<27>("v_and_b32 literal", cus, w, iters);
         run<28>("v_xor_b32 sgpr", cus, w, iters);
@@ -120,6 +131,14 @@ int main() {
         run<10>("v_xor_b32 (asm)", cus, w, iters);
         run<23>("v_bitop3_b32 (asm)", cus, w, iters);
         run<2>("v_perm_b32", cus, w, iters);
+        run<34>("v_mov_b32_sdwa preserve", cus, w, iters);
+        run<35>("v_lshlrev_b32_sdwa", cus, w, iters);
+        run<36>("v_or_b32_sdwa", cus, w, iters);
+        run<37>("v_perm_b32 (asm)", cus, w, iters);
+        run<38>("v_alignbit_b32 (asm)", cus, w, iters);
+        run<39>("v_add_u32 literal", cus, w, iters);
+        run<40>("v_mov_b32_sdwa pad", cus, w, iters);
+        run<41>("v_pk_add_u16", cus, w, iters);
     }
     return 0;
 }
