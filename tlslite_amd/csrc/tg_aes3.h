@@ -120,14 +120,11 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_DES_ANDOR     3DES SP-box address by v_and_or_b32 instead of v_bitop3
 //   TG_AB_OPEN_QUAD     AES open decrypt on the quad layout (open_dec_kernel, round 1) instead of
 //                       one lane per block (open_aes_kernel)
-//   TG_AB_PAIR       cipher phase with 2 lanes per chain (cbc_pair_kernel) when a CU gets at least
-//                    C3_CHAINS chains; TG_AB_PAIR_WAVES / TG_AB_PAIR_WAVES_MANY its waves per CU
-#ifndef TG_AB_PAIR_WAVES
-#define TG_AB_PAIR_WAVES 8
-#endif
-#ifndef TG_AB_PAIR_WAVES_MANY
-#define TG_AB_PAIR_WAVES_MANY 16
-#endif
+//   TG_AB_NO_PAIR    cipher phase on the quad layout (cbc_kernel) in the throughput regimes too,
+//                    instead of 2 lanes per chain (cbc_pair_kernel)
+//   TG_AB_PAIR_G1 / TG_AB_PAIR_GM  the pair kernel's prefetch group (blocks) in the one-generation
+//                    (cfg2) / many-chains (cfg3) regime; TG_AB_PAIR_MAC_MANY: the 128-VGPR MAC
+//                    kernel in the one-generation pair regime too
 #ifndef TG_AB_MAC_PRIO
 #define TG_AB_MAC_PRIO 0
 #endif
@@ -268,45 +265,47 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
             nxt[d][L] = ldg16(PL[L] + 64 * min((uint32_t)d, NL[L]));
 #endif
         }
-    for (uint32_t c = 0; c < nmax; c++) {
-        uint4 cur[4];
+    // The loop is unrolled by PF with ring slot k fixed per unrolled step: slot k's chunk is
+    // transposed out first and its registers reloaded straight away, so no register copies
+    // rotate the ring (they were 32 v_mov per chunk, ~4 % of the MAC phase's issue cycles).
+    for (uint32_t c0 = 0; c0 < nmax; c0 += PF) {
 #pragma unroll
-        for (int L = 0; L < 4; L++) cur[L] = nxt[0][L];
-#pragma unroll
-        for (int d = 0; d + 1 < PF; d++)
-#pragma unroll
-            for (int L = 0; L < 4; L++) nxt[d][L] = nxt[d + 1][L];
+        for (int k = 0; k < PF; k++) {
+            const uint32_t c = c0 + k;
+            if (c >= nmax) break;
+            // component t of lane p's piece of record L = record L's word 4p + t
+            uint32_t d[16], x[4];
+            x[0] = nxt[k][0].x; x[1] = nxt[k][1].x; x[2] = nxt[k][2].x; x[3] = nxt[k][3].x;
+            quad_transpose4(x, q);
+            d[0] = x[0]; d[4] = x[1]; d[8] = x[2]; d[12] = x[3];
+            x[0] = nxt[k][0].y; x[1] = nxt[k][1].y; x[2] = nxt[k][2].y; x[3] = nxt[k][3].y;
+            quad_transpose4(x, q);
+            d[1] = x[0]; d[5] = x[1]; d[9] = x[2]; d[13] = x[3];
+            x[0] = nxt[k][0].z; x[1] = nxt[k][1].z; x[2] = nxt[k][2].z; x[3] = nxt[k][3].z;
+            quad_transpose4(x, q);
+            d[2] = x[0]; d[6] = x[1]; d[10] = x[2]; d[14] = x[3];
+            x[0] = nxt[k][0].w; x[1] = nxt[k][1].w; x[2] = nxt[k][2].w; x[3] = nxt[k][3].w;
+            quad_transpose4(x, q);
+            d[3] = x[0]; d[7] = x[1]; d[11] = x[2]; d[15] = x[3];
 #ifdef TG_AB_MAC_NOLOAD
 #pragma unroll
-        for (int L = 0; L < 4; L++) nxt[PF - 1][L] = make_uint4(cur[L].y + c, cur[L].z ^ c, cur[L].w, cur[L].x);
+            for (int L = 0; L < 4; L++)
+                nxt[k][L] = make_uint4(nxt[k][L].y + c, nxt[k][L].z ^ c, nxt[k][L].w, nxt[k][L].x);
 #else
 #pragma unroll
-        for (int L = 0; L < 4; L++) nxt[PF - 1][L] = ldg16(PL[L] + 64 * min(c + PF, NL[L]));
+            for (int L = 0; L < 4; L++) nxt[k][L] = ldg16(PL[L] + 64 * min(c + PF, NL[L]));
 #endif
-        // component t of lane p's piece of record L = record L's word 4p + t
-        uint32_t d[16], x[4];
-        x[0] = cur[0].x; x[1] = cur[1].x; x[2] = cur[2].x; x[3] = cur[3].x;
-        quad_transpose4(x, q);
-        d[0] = x[0]; d[4] = x[1]; d[8] = x[2]; d[12] = x[3];
-        x[0] = cur[0].y; x[1] = cur[1].y; x[2] = cur[2].y; x[3] = cur[3].y;
-        quad_transpose4(x, q);
-        d[1] = x[0]; d[5] = x[1]; d[9] = x[2]; d[13] = x[3];
-        x[0] = cur[0].z; x[1] = cur[1].z; x[2] = cur[2].z; x[3] = cur[3].z;
-        quad_transpose4(x, q);
-        d[2] = x[0]; d[6] = x[1]; d[10] = x[2]; d[14] = x[3];
-        x[0] = cur[0].w; x[1] = cur[1].w; x[2] = cur[2].w; x[3] = cur[3].w;
-        quad_transpose4(x, q);
-        d[3] = x[0]; d[7] = x[1]; d[11] = x[2]; d[15] = x[3];
 #ifdef TG_AB_MAC_LOADONLY
-        if (c < nfull) {
-            uint32_t a = 0;
+            if (c < nfull) {
+                uint32_t a = 0;
 #pragma unroll
-            for (int i = 0; i < 16; i++) a ^= d[i];
-            mac.h[0] ^= a;
-        }
+                for (int i = 0; i < 16; i++) a ^= d[i];
+                mac.h[0] ^= a;
+            }
 #else
-        if (c < nfull) mac.update(d);
+            if (c < nfull) mac.update(d);
 #endif
+        }
     }
 }
 
@@ -600,52 +599,69 @@ __device__ __forceinline__ void pair_block(const PairAes& aes, const uint32_t* k
     vb = b;
 }
 
-template <int NR, bool AL, bool CLAMP>
-__device__ __forceinline__ void pcbc_group8(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
-                                            const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
-                                            uint8_t* O, uint32_t b0, uint32_t last, uint2 f[8]) {
-    uint2 c[8];
+// Pair-kernel configurations (same-box A/Bs, profiles/r03/ab_pair_r03*.txt):
+//   one generation (a CU gets exactly one workgroup of chains, cfg2): 8 waves, 8-block
+//   prefetch groups (103 VGPRs; one 168-VGPR MAC wave per SIMD beside the two cipher
+//   waves): cfg2 824 -> 855 GiB/s.  4-block groups (87 VGPRs) let a second MAC wave in,
+//   which slows the cipher phase -- the step's critical path -- more than it helps (794).
+//   many chains (cfg3): 8 waves, 4-block groups (95 VGPRs for AES-256) + two 128-VGPR MAC
+//   waves per SIMD (the MAC phase is that regime's critical path): cfg3 523 -> 540 GiB/s.
+constexpr int PAIR_WAVES = 8;
+#ifndef TG_AB_PAIR_G1
+#define TG_AB_PAIR_G1 8
+#endif
+#ifndef TG_AB_PAIR_GM
+#define TG_AB_PAIR_GM 4
+#endif
+
+template <int NR, int G, bool AL, bool CLAMP>
+__device__ __forceinline__ void pcbc_group(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
+                                           const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
+                                           uint8_t* O, uint32_t b0, uint32_t last, uint2 f[G]) {
+    constexpr int PAIR_G = G;
+    uint2 c[PAIR_G];
 #pragma unroll
-    for (int i = 0; i < 8; i++) c[i] = f[i];
+    for (int i = 0; i < PAIR_G; i++) c[i] = f[i];
     if constexpr (CLAMP) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const uint32_t b = b0 + 8 + i;
+        for (int i = 0; i < PAIR_G; i++) {
+            const uint32_t b = b0 + PAIR_G + i;
             f[i] = ld64t<AL>(P + 16 * (b < last ? b : last));
         }
     } else {
-        const uint8_t* Pn = P + 16 * (b0 + 8);
+        const uint8_t* Pn = P + 16 * (b0 + PAIR_G);
 #pragma unroll
-        for (int i = 0; i < 8; i++) f[i] = ld64t<AL>(Pn + 16 * i);
+        for (int i = 0; i < PAIR_G; i++) f[i] = ld64t<AL>(Pn + 16 * i);
     }
     uint8_t* Ob = O + 16 * b0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < PAIR_G; i++) {
         pair_block<NR>(aes, kw, ka, kb, va, vb, c[i].x, c[i].y);
         st64t<AL>(Ob + 16 * i, va, vb);
     }
 }
 
-template <int NR, bool AL>
+template <int NR, int GI, bool AL>
 __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
                                           const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
                                           uint8_t* O, uint32_t nb) {
     if (nb == 0) return;
+    constexpr uint32_t G = GI;
     const uint32_t last = nb - 1;
-    uint2 f[8];
+    uint2 f[G];
 #pragma unroll
-    for (int i = 0; i < 8; i++) f[i] = ld64t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
+    for (int i = 0; i < (int)G; i++) f[i] = ld64t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
     uint32_t b0 = 0;
-    if (nb >= 16) {  // first group peeled, as cbc_bulk
-        pcbc_group8<NR, AL, false>(aes, kw, ka, kb, va, vb, P, O, 0, last, f);
-        for (b0 = 8; b0 + 16 <= nb; b0 += 8) pcbc_group8<NR, AL, false>(aes, kw, ka, kb, va, vb, P, O, b0, last, f);
+    if (nb >= 2 * G) {  // first group peeled, as cbc_bulk
+        pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, P, O, 0, last, f);
+        for (b0 = G; b0 + 2 * G <= nb; b0 += G) pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, P, O, b0, last, f);
     }
-    if (b0 + 8 <= nb) {
-        pcbc_group8<NR, AL, true>(aes, kw, ka, kb, va, vb, P, O, b0, last, f);
-        b0 += 8;
+    if (b0 + G <= nb) {
+        pcbc_group<NR, GI, AL, true>(aes, kw, ka, kb, va, vb, P, O, b0, last, f);
+        b0 += G;
     }
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < (int)G; i++) {
         if (b0 + i < nb) {
             pair_block<NR>(aes, kw, ka, kb, va, vb, f[i].x, f[i].y);
             st64t<AL>(O + 16 * (b0 + i), va, vb);
@@ -653,7 +669,7 @@ __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw
     }
 }
 
-template <int NR, int WAVES>
+template <int NR, int WAVES, int G>
 __global__ void __launch_bounds__(64 * WAVES, 1)
 cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
                 uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
@@ -696,8 +712,8 @@ cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const
             }
             uint8_t* O = B + E + 8 * h;
             const uint32_t nb = n >> 4;
-            if (al) pcbc_bulk<NR, true>(aes, kw, ka, kb, va, vb, P, O, nb);
-            else pcbc_bulk<NR, false>(aes, kw, ka, kb, va, vb, P, O, nb);
+            if (al) pcbc_bulk<NR, G, true>(aes, kw, ka, kb, va, vb, P, O, nb);
+            else pcbc_bulk<NR, G, false>(aes, kw, ka, kb, va, vb, P, O, nb);
             // tail blocks from the MAC kernel's slot (8-byte aligned)
             const uint32_t r16 = n & 15;
             const uint8_t* slot = tails + (size_t)r * TAIL_SLOT + 8 * h;

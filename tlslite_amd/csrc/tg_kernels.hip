@@ -372,13 +372,30 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
     hipLaunchKernelGGL((prefix_kernel<CID, MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains,
                        recs, states, wire_len, meta, nrecords, epoch, sb.wire_cap);
     const dim3 grid((r1 - r0 + 255) / 256);
-    if (NR != 0 && many_chains(nchains))
+#ifdef TG_AB_PAIR_MAC_MANY
+    const bool mac_many = NR != 0 && nchains >= (uint32_t)C3_CHAINS * cu_count();
+#else
+    const bool mac_many = NR != 0 && many_chains(nchains);
+#endif
+    // (many chains: two 128-VGPR MAC waves per SIMD fit beside the cipher waves)
+    if (mac_many)
         hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS, MAC_LB_MANY, MAC_PF_MANY>), grid, dim3(256), 0, s, recs, r1, pt,
                            wire, states, wire_len, meta, tails, epoch, r0);
     else
         hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS>), grid, dim3(256), 0, s, recs, r1, pt, wire, states, wire_len,
                            meta, tails, epoch, r0);
     return hipGetLastError();
+}
+
+// The AES cipher phase runs 2 lanes per chain (cbc_pair_kernel) when every CU gets at
+// least a full workgroup of chains (C3_CHAINS = 256: cfg2, cfg3), the quad layout
+// (cbc_kernel, latency form) with fewer (cfg4's 2-16 chains per CU).
+static bool pair_regime(uint32_t nchains) {
+#ifdef TG_AB_NO_PAIR
+    return false;
+#else
+    return nchains >= (uint32_t)C3_CHAINS * cu_count();
+#endif
 }
 
 // phase 2 (stream s2, after phase 1): CBC over [explicit IV | P blocks | tail]
@@ -399,23 +416,21 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         return hipGetLastError();
     } else {
         const bool many = many_chains(nchains);
-#ifdef TG_AB_PAIR
-        if (nchains >= (uint32_t)C3_CHAINS * ncu) {
-            // throughput regimes: 2 lanes per chain (cbc_pair_kernel)
-            constexpr uint32_t W1 = TG_AB_PAIR_WAVES, WM = TG_AB_PAIR_WAVES_MANY;
-            const uint32_t pwg = many ? 32u * WM : 32u * W1;
+        if (pair_regime(nchains)) {
+            // a CU gets at least a workgroup's worth of chains: 2 lanes per chain
+            constexpr uint32_t pwg = 32u * PAIR_WAVES;
             uint32_t cpw = (nchains + ncu - 1) / ncu;
             cpw = cpw > pwg ? pwg : cpw;
-            auto kern = many ? cbc_pair_kernel<NR, WM> : cbc_pair_kernel<NR, W1>;
+            auto kern = many ? cbc_pair_kernel<NR, PAIR_WAVES, TG_AB_PAIR_GM>
+                             : cbc_pair_kernel<NR, PAIR_WAVES, TG_AB_PAIR_G1>;
             hipError_t e = set_lds(kern, AES_LDS_BYTES);
             if (e != hipSuccess) return e;
             uint32_t grid = (nchains + cpw - 1) / cpw;
             grid = grid > ncu ? ncu : grid;
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (many ? WM : W1)), AES_LDS_BYTES, s, chains, nchains, recs,
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PAIR_WAVES), AES_LDS_BYTES, s, chains, nchains, recs,
                                nrecords, pt, wire, states, meta, tails, cpw, epoch);
             return hipGetLastError();
         }
-#endif
         const uint32_t wg_chains = many ? 16u * C3_WAVES_MANY : (uint32_t)C3_CHAINS;
         uint32_t cpw = (nchains + ncu - 1) / ncu;
         cpw = cpw < 1 ? 1 : (cpw > wg_chains ? wg_chains : cpw);
@@ -444,12 +459,10 @@ std::string seal_cipher_kernel(uint32_t variant, uint32_t nchains) {
     const uint32_t ncu = cu_count();
     const bool many = many_chains(nchains);
     char b[64];
-#ifdef TG_AB_PAIR
-    if (nchains >= (uint32_t)C3_CHAINS * ncu) {
-        snprintf(b, sizeof b, "cbc_pair_kernel<%d, %d>", nr, many ? TG_AB_PAIR_WAVES_MANY : TG_AB_PAIR_WAVES);
+    if (pair_regime(nchains)) {
+        snprintf(b, sizeof b, "cbc_pair_kernel<%d, %d, %d>", nr, PAIR_WAVES, many ? TG_AB_PAIR_GM : TG_AB_PAIR_G1);
         return b;
     }
-#endif
     const uint32_t cpw = (nchains + ncu - 1) / ncu;
     if (many) snprintf(b, sizeof b, "cbc_kernel<%d, false, %d>", nr, C3_WAVES_MANY);
     else snprintf(b, sizeof b, "cbc_kernel<%d, %s>", nr, cpw < (uint32_t)C3_CHAINS ? "true" : "false");

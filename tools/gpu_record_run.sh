@@ -1,10 +1,12 @@
 #!/bin/bash
-# r02final4: the final round-2 tree on one MI355X -- full GPU tests, smoke, every bench
-# config, a 2-rank torchrun of bench.py (both ranks on this box's one GPU), and rocprofv3
+# The record run of a round on one MI355X -- full GPU tests, smoke, every bench config, a
+# 2-rank torch.distributed.run launch of bench.py (both ranks on this box's one GPU: the
+# launcher's env contract and the shard rendezvous, not a scaling number), and rocprofv3
 # kernel-trace statistics of each config.  Stops at the first failure.
+#   bash tools/gpu_record_run.sh <tag>     (outputs under gpurun_out/<tag>)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r02final4
+O=$R/gpurun_out/${1:-record}
 mkdir -p $O
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }

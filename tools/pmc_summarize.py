@@ -21,7 +21,7 @@ import sys
 
 out, cfg = sys.argv[1], sys.argv[2]
 SETUP = ("fill_kernel", "__amd_rocclr_fillBuffer")  # bench set-up / memsets, not the seal call
-DOMINANT = ("cbc_kernel", "lseal_kernel", "rc4_seal_kernel", "tdes4_kernel")
+DOMINANT = ("cbc_pair_kernel", "cbc_kernel", "rc4_seal_kernel", "tdes4_kernel")
 
 
 def stem(name):

@@ -7,6 +7,9 @@
 //   wrquad   cbc_kernel's stores, same pattern
 //   rdcoop   mac_kernel's cooperative loads: per instruction a quad reads 64 contiguous
 //            bytes of one of its 4 records (lane q: bytes [16q, 16q+16))
+//   rdstate / rdstate2 / rdstate64  scattered narrow reads of 2 KiB connection states (one lane
+//            per state: a few dwords of one / two 64-B sectors, or one whole sector as dwordx4):
+//            payload = 64 B per sector touched, NSTATE states (1 GiB span)
 // Each kernel moves exactly BYTES (reads) or BYTES (writes) of payload once.
 //   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/traffic_calib.hip -o traffic_calib
 #include <hip/hip_runtime.h>
@@ -64,6 +67,36 @@ __global__ void __launch_bounds__(256) rdcoop(const uint8_t* __restrict__ p, uin
     if (a == 0x12345678u) out[0] = a;
 }
 
+// scattered narrow loads (prefix_kernel / cipher-kernel state reads): one lane per 2 KiB
+// connection state, a few dwords of its first 64 bytes (one 64-B sector touched per lane);
+// payload counted as 64 B per lane
+constexpr size_t NSTATE = 1u << 19;
+__global__ void __launch_bounds__(256) rdstate(const uint8_t* __restrict__ p, uint32_t* out) {
+    const size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= NSTATE) return;
+    const uint32_t* s = (const uint32_t*)(p + r * 2048);
+    const uint32_t a = s[0] ^ s[4] ^ s[6] ^ s[9] ^ s[12];
+    if (a == 0x12345678u) out[0] = a;
+}
+// the same, two sectors per lane (bytes 0..63 and 128..191 of the state)
+__global__ void __launch_bounds__(256) rdstate2(const uint8_t* __restrict__ p, uint32_t* out) {
+    const size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= NSTATE) return;
+    const uint32_t* s = (const uint32_t*)(p + r * 2048);
+    const uint32_t a = s[0] ^ s[4] ^ s[33] ^ s[40];
+    if (a == 0x12345678u) out[0] = a;
+}
+// one full 64-B sector per lane as 4 x dwordx4 (the round keys of a state), 2 KiB apart
+__global__ void __launch_bounds__(256) rdstate64(const uint8_t* __restrict__ p, uint32_t* out) {
+    const size_t r = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= NSTATE) return;
+    const uint4* s = (const uint4*)(p + r * 2048 + 256);
+    uint32_t a = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) a ^= s[i].x + s[i].y + s[i].z + s[i].w;
+    if (a == 0x12345678u) out[0] = a;
+}
+
 int main() {
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -78,6 +111,9 @@ int main() {
         hipLaunchKernelGGL(rdquad, dim3(cus), dim3(1024), 0, 0, buf, out);
         hipLaunchKernelGGL(wrquad, dim3(cus), dim3(1024), 0, 0, buf);
         hipLaunchKernelGGL(rdcoop, dim3((NREC + 255) / 256), dim3(256), 0, 0, buf, out);
+        hipLaunchKernelGGL(rdstate, dim3(NSTATE / 256), dim3(256), 0, 0, buf, out);
+        hipLaunchKernelGGL(rdstate2, dim3(NSTATE / 256), dim3(256), 0, 0, buf, out);
+        hipLaunchKernelGGL(rdstate64, dim3(NSTATE / 256), dim3(256), 0, 0, buf, out);
     }
     (void)hipDeviceSynchronize();
     printf("done\n");

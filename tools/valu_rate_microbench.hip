@@ -60,6 +60,23 @@ __device__ __forceinline__ uint32_t op(uint32_t a, uint32_t b, uint32_t c) {
     return 0;
 }
 
+// mixed streams: chains 0..3 run op A, chains 4..7 op B (does a 4-cycle op issue beside
+// 2-cycle ops, or do their costs add?)
+template <int KIND>
+__device__ __forceinline__ uint32_t mixop(int i, uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    if (i < 4) {
+        if constexpr (KIND == 60 || KIND == 64) asm volatile("v_alignbit_b32 %0, %1, %1, 27" : "=v"(r) : "v"(a));
+        if constexpr (KIND == 61) asm volatile("v_perm_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+        if constexpr (KIND == 62) asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+        if constexpr (KIND == 63) asm volatile("v_xor_b32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(r) : "v"(a), "v"(b));
+    } else {
+        if constexpr (KIND == 64) asm volatile("v_alignbit_b32 %0, %1, %1, 27" : "=v"(r) : "v"(a));
+        else asm volatile("v_xor_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    }
+    return r;
+}
+
 template <int KIND>
 __global__ void __launch_bounds__(1024) rate_kernel(uint32_t* out, uint64_t* cyc, int iters, uint32_t seed) {
     uint32_t x[8];
@@ -74,7 +91,8 @@ __global__ void __launch_bounds__(1024) rate_kernel(uint32_t* out, uint64_t* cyc
         for (int r = 0; r < 8; r++)
 #pragma unroll
             for (int i = 0; i < 8; i++)
-                x[i] = op<KIND>(x[i], x[i ^ 4], (KIND == 3 || KIND == 13 || KIND == 14 || (KIND >= 18 && KIND != 31 && KIND < 34) || KIND == 37) ? x[(i + 2) & 7] : KIND == 31 ? (c & 7) : c);
+                if constexpr (KIND >= 60) x[i] = mixop<KIND>(i, x[i], x[i ^ 4], c ^ x[(i + 2) & 7]);
+                else x[i] = op<KIND>(x[i], x[i ^ 4], (KIND == 3 || KIND == 13 || KIND == 14 || (KIND >= 18 && KIND != 31 && KIND < 34) || KIND == 37) ? x[(i + 2) & 7] : KIND == 31 ? (c & 7) : c);
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     uint32_t s = 0;
@@ -119,7 +137,7 @@ int main() {
     int cus = 0;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
     const int iters = 4096;
-    for (int w : {1, 4}) {
+    for (int w : {2, 4}) {
         run<26>("v_lshrrev_b32 const", cus, w, iters);
         run<27>("v_and_b32 literal", cus, w, iters);
         run<28>("v_xor_b32 sgpr", cus, w, iters);
@@ -139,6 +157,11 @@ int main() {
         run<39>("v_add_u32 literal", cus, w, iters);
         run<40>("v_mov_b32_sdwa pad", cus, w, iters);
         run<41>("v_pk_add_u16", cus, w, iters);
+        run<60>("mix alignbit | xor", cus, w, iters);
+        run<61>("mix perm | xor", cus, w, iters);
+        run<62>("mix add3 | xor", cus, w, iters);
+        run<63>("mix xor_dpp | xor", cus, w, iters);
+        run<64>("alignbit (mix ref)", cus, w, iters);
     }
     return 0;
 }
