@@ -118,6 +118,8 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_WAVES_MANY    cipher waves per CU in the many-chains configuration (default 12)
 //   TG_AB_MAC_FLAT      cooperative MAC loads as flat_load (generic pointers) instead of global_load
 //   TG_AB_DES_ANDOR     3DES SP-box address by v_and_or_b32 instead of v_bitop3
+//   TG_AB_DES_OLD       tdes4_kernel on the 32-copy SP tables (v_alignbit + v_bitop3 per lookup)
+//                       instead of the byte-row tables (v_perm for the even lookups)
 //   TG_AB_OPEN_QUAD     AES open decrypt on the quad layout (open_dec_kernel, round 1) instead of
 //                       one lane per block (open_aes_kernel)
 //   TG_AB_NO_PAIR    cipher phase on the quad layout (cbc_kernel) in the throughput regimes too,
@@ -534,7 +536,7 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
     const uint32_t fiv = st->fixed_iv[q];
     const uint32_t E = st->explicit_iv ? 16u : 0u;
     bool any = false;
-    QuadAes::round_keys<NR>(st->ek, q, k);
+    QuadAes::round_keys<NR, LAT>(st->ek, q, k);
     for (uint32_t j = 0; j < ch.count; j++) {
         const uint32_t r = ch.first + j;
         if (r >= nrecords) break;
@@ -750,10 +752,39 @@ cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const
 constexpr int D4_THREADS = 512;
 constexpr int D4_CHAINS = D4_THREADS / 4;
 
-struct Des4 {
-    uint32_t be, bo, se, so, m;
+// Round 3 table layout for tdes4_kernel ("byte rows"): the even S-boxes' 6-bit index is
+// the low 6 bits of byte j of w = r ^ k_even (DesSP's rotated domain), so a table with one
+// row per BYTE value (the index replicated over the byte's two top bits) is addressed by
+// one v_perm (byte j of w -> address bits 8..15 | the lane's column) instead of v_alignbit +
+// v_bitop3.  Row stride 256 B = 8 tables x 8 lane copies x 4 B: table slot s (0..3: the
+// even-path tables 7,5,3,1 of lanes j = 0..3; 4..7: the odd-path tables 6,4,2,0), copy =
+// the chain's index in its half-wave, so the 32 lanes of a half-wave hit banks 8j + copy:
+// conflict-free.  The odd path's index (bits 8j+4..8j+9 of t = r ^ rotl4(k_odd)) is not
+// byte-aligned: v_alignbit puts it at bits 8..13 and a v_bitop3 masks it (rows 0..63).
+// 64 KiB, as the 32-copy layout.
+__device__ __forceinline__ void des_lds_fill_rows(uint32_t* lds) {
+    for (uint32_t idx = threadIdx.x; idx < 16384; idx += blockDim.x) {
+        const uint32_t row = idx >> 6, slot = (idx >> 3) & 7;
+        const uint32_t K = slot < 4 ? 7 - 2 * slot : 6 - 2 * (slot - 4);
+        lds[idx] = c_des.sp[K][row & 63];
+    }
+}
+// ROWS: the byte-row table layout above (des_lds_fill_rows); else the 32-copy layout of
+// des_lds_fill (rows of 6-bit indices, v_alignbit + v_bitop3 per lookup)
+template <bool ROWS>
+struct Des4T {
+    uint32_t be, bo, se, so, m;  // ROWS: se = the v_perm selector of the even lookup
     __device__ __forceinline__ void init() {
         const uint32_t lane = __lane_id(), j = lane & 3;
+        if constexpr (ROWS) {
+            const uint32_t copy = (lane >> 2) & 7;
+            m = vconst(0x3f00u);
+            be = (j * 8 + copy) * 4;
+            bo = ((4 + j) * 8 + copy) * 4;
+            se = 0x0c0c0000u | ((4u + j) << 8);  // address byte 1 <- byte j of w, byte 0 <- be
+            so = (8 * j + 28u) & 31u;            // t bits 8j+4 .. 8j+9 -> bits 8..13
+            return;
+        }
         m = vconst(0x1f80u);
         be = (lane & 31) * 4 + (7 - 2 * j) * 8192;
         bo = (lane & 31) * 4 + (6 - 2 * j) * 8192;
@@ -763,6 +794,13 @@ struct Des4 {
     }
     // Feistel f of te = r ^ k_even, to = r ^ rotl4(k_odd), summed over the quad
     __device__ __forceinline__ uint32_t f(uint32_t te, uint32_t to) const {
+        if constexpr (ROWS) {
+            const uint32_t uo = __builtin_amdgcn_alignbit(to, to, so);
+            uint32_t v = lds_read32(perm(te, be, se)) ^ lds_read32(__builtin_amdgcn_bitop3_b32(uo, m, bo, 0xEA));
+            v ^= quad_dpp<0xB1>(v);
+            v ^= quad_dpp<0x4E>(v);
+            return v;
+        }
         const uint32_t ue = __builtin_amdgcn_alignbit(te, te, se);
         const uint32_t uo = __builtin_amdgcn_alignbit(to, to, so);
 #ifdef TG_AB_DES_ANDOR
@@ -814,6 +852,12 @@ struct Des4 {
         iv1 = bswap32(lo);
     }
 };
+using Des4 = Des4T<false>;
+#ifdef TG_AB_DES_OLD
+constexpr bool DES_ROWS = false;
+#else
+constexpr bool DES_ROWS = true;
+#endif
 
 __global__ void __launch_bounds__(D4_THREADS, 1)
 tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
@@ -822,7 +866,8 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
              uint32_t cpw, uint32_t epoch) {
     // SP tables at LDS offset 0 (the kernel's only LDS), read back by absolute address (Des4::f)
     extern __shared__ __attribute__((aligned(16))) uint32_t d4_lds[];
-    des_lds_fill(d4_lds);
+    if constexpr (DES_ROWS) des_lds_fill_rows(d4_lds);
+    else des_lds_fill(d4_lds);
     __syncthreads();
     const uint32_t j = threadIdx.x & 3;
     const uint32_t local = threadIdx.x >> 2;
@@ -830,7 +875,7 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
     if (local >= cpw || cid >= nchains) return;  // the 4 lanes of a chain leave together
     const tlsgpu_chain ch = chains[cid];
     ConnState* st = states + ch.state;
-    Des4 D;
+    Des4T<DES_ROWS> D;
     D.init();
     uint32_t ke[48], ko[48];
 #pragma unroll

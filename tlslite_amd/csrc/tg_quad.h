@@ -61,38 +61,44 @@ struct QuadAes {
     // and the round key rides in that inner term: k2 is the key column of lane q+2 (round_keys()),
     // so once the T0/T1 lookups return only two dependent DPP XORs remain (a chain needs four).
     // The T2/T3 lookups are issued first: they feed the inner term.
-    // LAT (the few-chains regime, a lone wave per SIMD): the last step as v_mov_dpp of u +
-    // a plain 3-input XOR.  A DPP instruction that reads a VGPR written by the instruction
-    // just before it (z) needs two wait states, so the fused v_xor_b32_dpp puts an s_nop on
-    // the round's critical path; w is moved while the T0/T1 lookups are still in flight
-    // (the scheduling barrier keeps it there), and the XOR is a v_bitop3 because a plain ^
-    // would be folded back into v_xor_b32_dpp.  cfg4: 129.6 -> 125.9 ms.  With 16 waves
-    // per CU (cfg2, cfg3) the extra VALU instruction costs more than the latency it saves
-    // (cfg3 cipher phase 2.18 -> 2.24 ms), so the throughput form keeps the fused DPP.
+    //
+    // LAT (the few-chains regime, a lone wave per SIMD, cfg4): w = dpp2(u) is moved while the
+    // T0/T1 lookups are still in flight (the scheduling barrier keeps it there; a DPP reading
+    // a VGPR written just before needs two wait states, which a fused v_xor_b32_dpp would put
+    // on the critical path: cfg4 129.6 -> 125.9 ms in round 2), and the round key goes into the
+    // LAST instruction instead, a 3-input XOR of z, w = dpp2(t2 ^ dpp1(t3)) and the lane's
+    // own key column: the T2/T3 half (issued first) is xor_dpp -> mov_dpp, hidden under
+    // the T0/T1 lookups, and only z = t0 ^ dpp1(t1) and the final v_bitop3 follow the last
+    // lookup.  Same 4 VALU as the throughput form (whose separate key XOR it drops).  For a
+    // lone wave (tools/aes_round_latency.hip, profiles/r03/round_latency_*.log) a dependent
+    // VALU step costs ~9 cycles, a DPP one ~12, an LDS lookup ~51: the round is ~106 cycles
+    // (cfg4/512 123.1 -> 122.3 ms).  Issuing the four address ops before the four reads
+    // (sched_group_barrier) made it 110.5 (128.2 ms): the reads interleaved with their
+    // addresses go out sooner.
     template <bool LAT>
-    __device__ __forceinline__ uint32_t round(uint32_t x, uint32_t k2) const {
+    __device__ __forceinline__ uint32_t round(uint32_t x, uint32_t k) const {
         const uint32_t t2 = look<2, 2>(x);
         const uint32_t t3 = look<3, 3>(x);
         const uint32_t t0 = look<0, 0>(x);
         const uint32_t t1 = look<1, 1>(x);
-        const uint32_t u = (t2 ^ k2) ^ quad_dpp<0x39>(t3);
-        if constexpr (!LAT) {
+        if constexpr (!LAT) {  // k = key column q+2 (round_keys<NR, false>)
+            const uint32_t u = (t2 ^ k) ^ quad_dpp<0x39>(t3);
             const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
             return z ^ quad_dpp<0x4E>(u);
-        } else {
-            const uint32_t w = quad_dpp<0x4E>(u);
+        } else {  // k = key column q (round_keys<NR, true>)
+            const uint32_t w = quad_dpp<0x4E>(t2 ^ quad_dpp<0x39>(t3));
             __builtin_amdgcn_sched_barrier(0);
             const uint32_t z = t0 ^ quad_dpp<0x39>(t1);
-            return __builtin_amdgcn_bitop3_b32(z, w, z, 0x3C);
+            return __builtin_amdgcn_bitop3_b32(z, w, k, 0x96);
         }
     }
     // per-lane round keys in the layout round()/last() expect: k[0] = whitening column q,
-    // k[r >= 1] = column (q+2)&3 of round key r
-    template <int NR>
+    // k[r >= 1] = column (q+2)&3 of round key r (throughput form) / column q (LAT)
+    template <int NR, bool LAT = false>
     static __device__ __forceinline__ void round_keys(const uint32_t* ek, uint32_t q, uint32_t* k) {
         k[0] = ek[q];
 #pragma unroll
-        for (int r = 1; r <= NR; r++) k[r] = ek[4 * r + ((q + 2) & 3)];
+        for (int r = 1; r <= NR; r++) k[r] = ek[4 * r + (LAT ? q : ((q + 2) & 3))];
     }
     template <bool LAT>
     __device__ __forceinline__ uint32_t last(uint32_t x, uint32_t k) const {
@@ -101,15 +107,15 @@ struct QuadAes {
         const uint32_t s3 = look<1, 3>(x) & 0xff000000u;
         const uint32_t s0 = look<2, 0>(x) & 0xffu;
         const uint32_t s1 = look<3, 1>(x) & 0xff00u;
-        const uint32_t u = (s2 ^ k) ^ quad_dpp<0x39>(s3);
         if constexpr (!LAT) {
+            const uint32_t u = (s2 ^ k) ^ quad_dpp<0x39>(s3);
             const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
             return z ^ quad_dpp<0x4E>(u);
         } else {
-            const uint32_t w = quad_dpp<0x4E>(u);
+            const uint32_t w = quad_dpp<0x4E>(s2 ^ quad_dpp<0x39>(s3));
             __builtin_amdgcn_sched_barrier(0);
             const uint32_t z = s0 ^ quad_dpp<0x39>(s1);
-            return __builtin_amdgcn_bitop3_b32(z, w, z, 0x3C);
+            return __builtin_amdgcn_bitop3_b32(z, w, k, 0x96);
         }
     }
     // one block of one chain
@@ -146,6 +152,9 @@ struct PairAes : QuadAes {
         const uint32_t a0 = look<0, 0>(a), b1 = look<1, 1>(b), b0 = look<0, 0>(b), a3 = look<3, 3>(a);
         const uint32_t sa = __builtin_amdgcn_bitop3_b32(a2, b3, ka, 0x96);  // partner's column 2h+2
         const uint32_t sb = __builtin_amdgcn_bitop3_b32(a1, b2, kb, 0x96);  // partner's column 2h+3
+        // (the partner's terms moved by v_mov_dpp ahead of the last lookups and one 3-input XOR
+        // per column after them -- a shorter dependent path, the same VALU count -- measured
+        // 3.5 % slower on cfg2, profiles/r03/ab_pair.txt: kept as v_xor + v_xor_dpp)
         a = (a0 ^ b1) ^ swap(sa);
         b = (b0 ^ a3) ^ swap(sb);
     }
