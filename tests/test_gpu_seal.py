@@ -449,3 +449,32 @@ def test_many_chains_vs_oracle(suite, version):
     bad = [c for c, (s, o) in enumerate(zip(states, conns)) if s.iv != o.iv or s.seqnum != o.seqnum]
     assert not bad, "chains with a wrong final state: %s" % bad[:10]
     wl.free()
+
+
+def test_library_workspaces_released_and_reallocated():
+    """tlsgpu_seal_dev with a NULL workspace on several short-lived streams, then
+    tlsgpu_release_workspaces (which frees the library-owned buffers after waiting for the
+    device), then more NULL-workspace seals: every batch equals the first (no state of a
+    freed buffer leaks into a later call)."""
+    _T()
+    from tlslite_amd import _native as N
+    from tlslite_amd import workloads as W
+    from tlslite_amd.device import Stream
+    from tlslite_amd.recordlayer import seal_dev
+    wl = W.cfg2(n=300, pt_len=3001, seed=31)
+    wl.to_device()
+    var, d_ch, nch = wl.launches[0]
+    outs = []
+    for k in range(6):
+        s = Stream()
+        wl.reset_states(s)
+        wl.d_wire.zero(s)
+        seal_dev(d_ch, nch, wl.d_recs, wl.n_records, wl.d_pt, wl.d_wire, wl.d_states, wl.d_len, var, None, s)
+        s.synchronize()
+        outs.append((wl.d_wire.download().tobytes(), wl.d_len.download().tobytes(), wl.d_states.download().tobytes()))
+        s.close()
+        if k == 2:
+            N.call("tlsgpu_release_workspaces")
+    assert all(o == outs[0] for o in outs)
+    N.call("tlsgpu_release_workspaces")
+    wl.free()

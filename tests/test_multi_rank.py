@@ -184,3 +184,37 @@ def test_two_rank_hip_sharding_matches_oracle(tmp_path):
     assert got[0] == dig(wire1)
     assert got[1] == dig(wire2)
     assert got[0] != got[1]
+
+
+def _rdzv_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from tlslite_amd.shard import ShardGroup, device_for_rank
+    g = ShardGroup()
+    out = {"max": g.max(10.0 - rank), "sum": g.sum(rank + 0.5),
+           "gather": g.gather_bytes(bytes([rank]) * (rank + 1)), "dev": device_for_rank(g.local, 2)}
+    for _ in range(5):
+        g.barrier()
+    g.close()
+    q.put((rank, out))
+
+
+def test_shard_rendezvous_three_ranks():
+    """The bench's rank plumbing without PyTorch (tlslite_amd.shard): 3 ranks, max / sum of
+    floats, an all-gather of different-length byte strings in rank order, repeated barriers,
+    and the rank -> device map (LOCAL_RANK % devices)."""
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rdzv_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(3):
+        assert res[r]["max"] == 10.0
+        assert res[r]["sum"] == 0.5 + 1.5 + 2.5
+        assert res[r]["gather"] == [b"\x00", b"\x01\x01", b"\x02\x02\x02"]
+        assert res[r]["dev"] == r % 2

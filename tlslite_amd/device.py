@@ -51,10 +51,13 @@ class Stream:
     def synchronize(self):
         N.call("tlsgpu_stream_synchronize", self.handle)
 
-    def __del__(self):
+    def close(self):
         if getattr(self, "_own", False) and self.handle:
             N.lib.tlsgpu_stream_destroy(self.handle)
             self.handle = ctypes.c_void_p(None)
+
+    def __del__(self):
+        self.close()
 
 
 class Event:

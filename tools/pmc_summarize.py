@@ -20,7 +20,10 @@ import statistics
 import sys
 
 out, cfg = sys.argv[1], sys.argv[2]
-SETUP = ("fill_kernel", "__amd_rocclr_fillBuffer")  # bench set-up / memsets, not the seal call
+NCU = 256
+# bench set-up: synthetic plaintext fill, buffer zeroing, state resets and the copy-rate
+# measurement (d2d copies) -- not the seal call
+SETUP = ("fill_kernel", "__amd_rocclr_fillBuffer", "__amd_rocclr_copyBuffer")
 DOMINANT = ("cbc_pair_kernel", "cbc_kernel", "rc4_seal_kernel", "tdes4_kernel")
 
 
@@ -31,8 +34,17 @@ def stem(name):
     return name.split("(")[0][:60]
 
 
+def read_bytes(row):
+    """HBM read bytes: exact from the request-size counters when collected, else the
+    FETCH_SIZE doubling calibrated for wide streaming reads."""
+    if "TCC_EA0_RDREQ_128B_sum" in row:
+        return int(32 * row.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * row.get("TCC_EA0_RDREQ_64B_sum", 0)
+                   + 128 * row["TCC_EA0_RDREQ_128B_sum"])
+    return int(2 * row.get("FETCH_SIZE", 0) * 1024)
+
+
 def hbm_bytes(row):
-    return int((2 * row.get("FETCH_SIZE", 0) + row.get("WRITE_SIZE", 0)) * 1024)
+    return read_bytes(row) + int(row.get("WRITE_SIZE", 0) * 1024)
 
 
 counters = {}   # stem -> counter -> {dispatch: value}
@@ -61,6 +73,15 @@ for k, cs in counters.items():
         row["duration_ms"] = statistics.median([x for x in ds if x >= 0.3 * top]) / 1e6
     if "FETCH_SIZE" in row or "WRITE_SIZE" in row:
         row["hbm_bytes"] = hbm_bytes(row)
+        row["read_bytes"] = read_bytes(row)
+        row["read_bytes_2xfetch"] = int(2 * row.get("FETCH_SIZE", 0) * 1024)
+    if row.get("duration_ms") and row.get("GRBM_GUI_ACTIVE"):
+        cyc = row["GRBM_GUI_ACTIVE"] / 8  # per XCD
+        row["clock_ghz"] = round(cyc / (row["duration_ms"] * 1e6), 3)
+        # SQ_LDS_IDX_ACTIVE: LDS-array cycles summed over CUs (2 per conflict-free ds_read_b32)
+        row["lds_busy"] = round(row.get("SQ_LDS_IDX_ACTIVE", 0) / NCU / cyc, 3)
+        # wave64 VALU instructions per SIMD per cycle (x 2.5-4.2 cycles each = VALU busy)
+        row["valu_inst_per_simd_cycle"] = round(row.get("SQ_INSTS_VALU", 0) / (4 * NCU) / cyc, 4)
     res["kernels"][k] = row
 
 seal = {k: r for k, r in res["kernels"].items() if not k.startswith(SETUP)}
@@ -71,9 +92,11 @@ res["hbm_bytes_per_launch"] = seal[dom].get("hbm_bytes") if dom else None
 res["hbm_bytes_per_launch_raw"] = (int((seal[dom].get("FETCH_SIZE", 0) + seal[dom].get("WRITE_SIZE", 0)) * 1024)
                                    if dom else None)
 res["seal_call_hbm_bytes"] = sum(r.get("hbm_bytes", 0) for r in seal.values())
-res["note"] = ("hbm_bytes_per_launch: the dominant kernel's (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch "
-               "(gfx950 FETCH_SIZE halves wide reads); seal_call_hbm_bytes: sum over the seal call's kernels; "
-               "set-up kernels (%s) excluded" % ", ".join(SETUP))
+res["note"] = ("hbm_bytes_per_launch: the dominant kernel's HBM bytes per launch = reads from the "
+               "request-size counters (32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B) + WRITE_SIZE*1024 "
+               "(read_bytes_2xfetch: the FETCH_SIZE doubling, exact only for wide streaming reads); "
+               "seal_call_hbm_bytes: sum over the seal call's kernels; set-up kernels (%s) excluded; "
+               "clock = GRBM_GUI_ACTIVE / 8 XCDs / duration" % ", ".join(SETUP))
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 with open(os.path.join(root, "profiles", "pmc_%s.json" % cfg), "w") as fh:
     json.dump(res, fh, indent=1)
