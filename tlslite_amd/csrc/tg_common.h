@@ -30,20 +30,22 @@ struct ConnState {
     uint32_t mac_key[8];   // SSL3-SHA1 MAC key, big-endian words (20 bytes used)
     uint32_t mac_key_len;
     uint32_t rc4_i, rc4_j;
-    uint32_t pad0[5];      // ek starts on a 64-B sector: the cipher kernels read 4 sectors of
-                           // round keys (AES-256) instead of 5 (cfg3: 64 MB less per call)
+    uint32_t pad0[21];     // ek starts on a 128-B line: HBM reads are 128-B requests even for
+                           // scattered narrow loads (tools/traffic_calib.hip), and the 240 B of
+                           // AES-256 round keys then take 2 lines instead of 3
     uint32_t ek[60];       // AES encryption round keys, LE column words
     uint32_t dk[60];       // AES equivalent-inverse-cipher round keys, LE column words
     uint32_t des[3][32];   // 3DES: per key, 16 rounds x {even-box word, odd-box word}
     uint8_t rc4_S[256];    // Python_RC4.S (python_rc4.py:21)
-    uint8_t reserved[TLSGPU_CONN_STATE_BYTES - 1312];
+    uint8_t reserved[TLSGPU_CONN_STATE_BYTES - 1376];
 };
-// Sector map (64 B): [0,64) everything prefix_kernel reads and the chain's CBC residue and
-// fixedIVBlock; [64,128) the HMAC midstates (mac_kernel); [192,432) the AES round keys.
+// Line map (128 B, the HBM request size): line 0 = everything prefix_kernel reads, the
+// chain's CBC residue and fixedIVBlock ([0,64)) and the HMAC midstates ([64,128), mac_kernel);
+// lines 2-3 = the AES round keys ([256,496)).  A cipher-kernel chain reads 3 lines.
 static_assert(__builtin_offsetof(ConnState, iv) == 32 && __builtin_offsetof(ConnState, fixed_iv) == 48,
               "prefix/cipher fields in the first sector");
 static_assert(__builtin_offsetof(ConnState, mac_in) == 64, "HMAC midstates in the second sector");
-static_assert(__builtin_offsetof(ConnState, ek) == 192, "round keys sector-aligned");
+static_assert(__builtin_offsetof(ConnState, ek) == 256, "round keys line-aligned");
 // the ABI blob (tlsgpu_conn_state) and the device struct must have the same stride
 static_assert(sizeof(ConnState) == TLSGPU_CONN_STATE_BYTES, "ConnState must be exactly 2048 bytes");
 

@@ -62,16 +62,9 @@ struct Hash<TLSGPU_MAC_SHA1> {
             f = bx3(s[1], s[2], s[3]);
             k = 0xCA62C1D6u;
         }
-#if defined(__HIP_DEVICE_COMPILE__) && defined(TG_AB_SHA_ADD2)
-        // A/B: four 2-cycle v_add_u32 (VOP2, K as a literal) instead of two 4-cycle v_add3_u32
-        uint32_t tmp, x, y;
-        asm volatile("v_add_u32 %0, %1, %2" : "=v"(x) : "i"(k), "v"(wt));
-        asm volatile("v_add_u32 %0, %1, %2" : "=v"(y) : "v"(x), "v"(s[4]));
-        asm volatile("v_add_u32 %0, %1, %2" : "=v"(x) : "v"(y), "v"(f));
-        asm volatile("v_add_u32 %0, %1, %2" : "=v"(tmp) : "v"(x), "v"(rotl32(s[0], 5)));
-#else
+        // two v_add3_u32 (4-cycle) -- four 2-cycle v_add_u32 measured 1-2 % slower on
+        // cfg2 / cfg3 (profiles/r03/ab_mac.txt)
         const uint32_t tmp = rotl32(s[0], 5) + f + s[4] + k + wt;
-#endif
         s[4] = s[3];
         s[3] = s[2];
         s[2] = rotl32(s[1], 30);
