@@ -567,8 +567,9 @@ def main():
                          "traffic_ratio_with_state": round(traffic / (alg_bytes + state_bytes), 3) if traffic else None,
                          "seal_call_hbm_bytes": seal_call_bytes,
                          "seal_call_ratio": round(seal_call_bytes / alg_bytes, 3) if seal_call_bytes else None,
-                         "traffic_note": "traffic / seal_call_hbm_bytes: PMC (2 FETCH_SIZE + WRITE_SIZE) of the "
-                                         "dominant kernel / of all kernels of one seal call "
+                         "traffic_note": "traffic / seal_call_hbm_bytes: PMC HBM bytes (reads from the "
+                                         "request-size counters 32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B, "
+                                         "+ WRITE_SIZE) of the dominant kernel / of all kernels of one seal call "
                                          "(profiles/pmc_<cfg>.json); ratios against alg_bytes (P read + 5+C "
                                          "written) and against alg_bytes + the cipher's per-connection state",
                          "lds": lds},
