@@ -609,6 +609,10 @@ __device__ __forceinline__ void pair_block(const PairAes& aes, const uint32_t* k
 //   many chains (cfg3): 8 waves, 4-block groups (95 VGPRs for AES-256) + two 128-VGPR MAC
 //   waves per SIMD (the MAC phase is that regime's critical path): cfg3 523 -> 540 GiB/s.
 constexpr int PAIR_WAVES = 8;
+#ifndef TG_AB_PAIR_WM
+#define TG_AB_PAIR_WM 8  // waves per CU in the many-chains regime
+#endif
+constexpr int PAIR_WAVES_MANY = TG_AB_PAIR_WM;
 #ifndef TG_AB_PAIR_G1
 #define TG_AB_PAIR_G1 8
 #endif

@@ -418,16 +418,17 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         const bool many = many_chains(nchains);
         if (pair_regime(nchains)) {
             // a CU gets at least a workgroup's worth of chains: 2 lanes per chain
-            constexpr uint32_t pwg = 32u * PAIR_WAVES;
+            const uint32_t waves = many ? PAIR_WAVES_MANY : PAIR_WAVES;
+            const uint32_t pwg = 32u * waves;
             uint32_t cpw = (nchains + ncu - 1) / ncu;
             cpw = cpw > pwg ? pwg : cpw;
-            auto kern = many ? cbc_pair_kernel<NR, PAIR_WAVES, TG_AB_PAIR_GM>
+            auto kern = many ? cbc_pair_kernel<NR, PAIR_WAVES_MANY, TG_AB_PAIR_GM>
                              : cbc_pair_kernel<NR, PAIR_WAVES, TG_AB_PAIR_G1>;
             hipError_t e = set_lds(kern, AES_LDS_BYTES);
             if (e != hipSuccess) return e;
             uint32_t grid = (nchains + cpw - 1) / cpw;
             grid = grid > ncu ? ncu : grid;
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * PAIR_WAVES), AES_LDS_BYTES, s, chains, nchains, recs,
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), AES_LDS_BYTES, s, chains, nchains, recs,
                                nrecords, pt, wire, states, meta, tails, cpw, epoch);
             return hipGetLastError();
         }
@@ -460,7 +461,8 @@ std::string seal_cipher_kernel(uint32_t variant, uint32_t nchains) {
     const bool many = many_chains(nchains);
     char b[64];
     if (pair_regime(nchains)) {
-        snprintf(b, sizeof b, "cbc_pair_kernel<%d, %d, %d>", nr, PAIR_WAVES, many ? TG_AB_PAIR_GM : TG_AB_PAIR_G1);
+        snprintf(b, sizeof b, "cbc_pair_kernel<%d, %d, %d>", nr, many ? PAIR_WAVES_MANY : PAIR_WAVES,
+                 many ? TG_AB_PAIR_GM : TG_AB_PAIR_G1);
         return b;
     }
     const uint32_t cpw = (nchains + ncu - 1) / ncu;
