@@ -228,7 +228,8 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state *st, uint32_t pt_len, uint32_t 
 size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords);
 /* Free every library-owned seal / open workspace (the NULL-workspace buffers, one per
  * (device, stream) ever used).  Waits for each device they live on first.  Callers that
- * create and destroy many streams call it; otherwise the buffers live until exit. */
+ * create and destroy many streams call it; otherwise the buffers live until exit.  Must
+ * not run concurrently with a seal / open call that passes a NULL workspace. */
 int tlsgpu_release_workspaces(void);
 /* Name of the cipher-phase kernel a seal call of `nchains` chains of `variant` runs on the
  * current device (its rocprofv3 name stem, e.g. "cbc_kernel<10, false>"): the layout is

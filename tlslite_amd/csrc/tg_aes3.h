@@ -109,6 +109,7 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_MAC_PRIO / TG_AB_CBC_PRIO  wave priorities of the MAC / cipher waves
 //   TG_AB_MAC_LOADONLY  cooperative MAC: loads + transposes, no compression (timing only)
 //   TG_AB_MAC_NOLOAD    cooperative MAC: compressions on register data, no loads (timing only)
+//   TG_AB_MAC_NOTRANS   cooperative MAC: no quad transposes (timing only: what they cost)
 //   TG_AB_MAC_PF        chunks the cooperative MAC loop prefetches (default 2)
 //   TG_AB_MAC_LB        mac_kernel's launch bound in 256-thread blocks per CU (default 3)
 //   TG_AB_OLD_ADDR      byte-1 T-table address by v_perm (as the other bytes) instead of v_bitop3
@@ -289,6 +290,12 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
             x[0] = nxt[k][0].w; x[1] = nxt[k][1].w; x[2] = nxt[k][2].w; x[3] = nxt[k][3].w;
             quad_transpose4(x, q);
             d[3] = x[0]; d[7] = x[1]; d[11] = x[2]; d[15] = x[3];
+#ifdef TG_AB_MAC_NOTRANS  // timing only: the loaded words as they are (wrong MACs)
+#pragma unroll
+            for (int L = 0; L < 4; L++) {
+                d[4 * L] = nxt[k][L].x; d[4 * L + 1] = nxt[k][L].y; d[4 * L + 2] = nxt[k][L].z; d[4 * L + 3] = nxt[k][L].w;
+            }
+#endif
 #ifdef TG_AB_MAC_NOLOAD
 #pragma unroll
             for (int L = 0; L < 4; L++)
