@@ -102,27 +102,22 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 }
 
 // Compile-time experiment switches (tools/build_ab.sh builds them into separate
-// libraries; the product build defines none):
-//   TG_AB_MAC_NT     MAC plaintext loads non-temporal
+// libraries; the product build defines none).  Variants measured slower and not kept
+// (non-temporal loads / stores, v_perm byte-1 addresses, v_cndmask transposes, flat
+// loads, v_and_or 3DES addresses) were removed in round 3; their results are in DESIGN.md
+// and profiles/r02/ab_summary.txt.
 //   TG_AB_NO_MAC     MAC bulk skipped (wrong MACs; timing of the cipher phase alone)
-//   TG_AB_CBC_NT_ST  ciphertext stores non-temporal
 //   TG_AB_MAC_PRIO / TG_AB_CBC_PRIO  wave priorities of the MAC / cipher waves
 //   TG_AB_MAC_LOADONLY  cooperative MAC: loads + transposes, no compression (timing only)
 //   TG_AB_MAC_NOLOAD    cooperative MAC: compressions on register data, no loads (timing only)
 //   TG_AB_MAC_NOTRANS   cooperative MAC: no quad transposes (timing only: what they cost)
 //   TG_AB_MAC_PF        chunks the cooperative MAC loop prefetches (default 2)
 //   TG_AB_MAC_LB        mac_kernel's launch bound in 256-thread blocks per CU (default 3)
-//   TG_AB_OLD_ADDR      byte-1 T-table address by v_perm (as the other bytes) instead of v_bitop3
-//   TG_AB_OLD_SEL       cooperative-load transposes select with v_cndmask instead of v_bitop3
 //   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
 //   TG_AB_NO_MANY       no many-chains configuration (12 cipher waves + 128-VGPR MAC kernel, cfg3)
 //   TG_AB_WAVES_MANY    cipher waves per CU in the many-chains configuration (default 12)
-//   TG_AB_MAC_FLAT      cooperative MAC loads as flat_load (generic pointers) instead of global_load
-//   TG_AB_DES_ANDOR     3DES SP-box address by v_and_or_b32 instead of v_bitop3
 //   TG_AB_DES_OLD       tdes4_kernel on the 32-copy SP tables (v_alignbit + v_bitop3 per lookup)
 //                       instead of the byte-row tables (v_perm for the even lookups)
-//   TG_AB_OPEN_QUAD     AES open decrypt on the quad layout (open_dec_kernel, round 1) instead of
-//                       one lane per block (open_aes_kernel)
 //   TG_AB_NO_PAIR    cipher phase on the quad layout (cbc_kernel) in the throughput regimes too,
 //                    instead of 2 lanes per chain (cbc_pair_kernel)
 //   TG_AB_PAIR_G1 / TG_AB_PAIR_GM  the pair kernel's prefetch group (blocks) in the one-generation
@@ -141,12 +136,7 @@ __device__ __forceinline__ void load64t(const uint8_t* p, uint32_t d[16]) {
     if constexpr (AL16) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-#ifdef TG_AB_MAC_NT
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 v = __builtin_nontemporal_load((const u32x4*)p + q);
-#else
             const uint4 v = ((const uint4*)p)[q];
-#endif
             d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
         }
     } else {
@@ -180,7 +170,7 @@ constexpr int MAC_PF = TG_AB_MAC_PF;  // chunks prefetched ahead by the cooperat
 // rebuilt from DPP-exchanged integers, which the compiler would otherwise turn into
 // flat_load (address space unknown)
 __device__ __forceinline__ uint4 ldg16(const uint8_t* p) {
-#if defined(TG_AB_MAC_FLAT) || !defined(__HIP_DEVICE_COMPILE__)
+#if !defined(__HIP_DEVICE_COMPILE__)
     return *(const uint4*)p;
 #else
     typedef __attribute__((address_space(1))) const uint32_t g_u32;
@@ -201,21 +191,6 @@ __device__ __forceinline__ uint32_t quad_lane(uint32_t v) {
 // q ^ 2 for 0x4E): of the register pair (a, b) the lane keeps the element whose index
 // bit equals its own bit `hi` and trades the other with the partner -- it sends exactly
 // the element it overwrites.  3 VALU per pair (the DPP rides in the selects).
-#ifdef TG_AB_OLD_SEL
-template <int CTRL>
-__device__ __forceinline__ void quad_bfly(uint32_t& a, uint32_t& b, bool hi) {
-    const uint32_t r = quad_dpp<CTRL>(hi ? a : b);
-    a = hi ? r : a;
-    b = hi ? b : r;
-}
-__device__ __forceinline__ void quad_transpose4(uint32_t x[4], uint32_t q) {
-    const bool b0 = (q & 1) != 0, b1 = (q & 2) != 0;
-    quad_bfly<0xB1>(x[0], x[1], b0);
-    quad_bfly<0xB1>(x[2], x[3], b0);
-    quad_bfly<0x4E>(x[0], x[2], b1);
-    quad_bfly<0x4E>(x[1], x[3], b1);
-}
-#else
 // the selects as v_bitop3 (m ? x : y, 2 cycles with all-VGPR operands) on a per-lane
 // all-ones / all-zeros mask instead of v_cndmask on a lane mask in SGPRs (4 cycles)
 template <int CTRL>
@@ -233,7 +208,6 @@ __device__ __forceinline__ void quad_transpose4(uint32_t x[4], uint32_t q) {
     quad_bfly<0x4E>(x[0], x[2], m1);
     quad_bfly<0x4E>(x[1], x[3], m1);
 }
-#endif
 
 // MAC over the 64-byte chunks of the quad's four records, loaded cooperatively: per load
 // instruction lane q fetches bytes [16q, 16q+16) of record L's chunk, so a quad reads a
@@ -427,11 +401,7 @@ __device__ __forceinline__ uint32_t ld32t(const uint8_t* p) {
 template <bool AL>
 __device__ __forceinline__ void st32t(uint8_t* p, uint32_t v) {
     if constexpr (AL) {
-#ifdef TG_AB_CBC_NT_ST
-        __builtin_nontemporal_store(v, (uint32_t*)p);
-#else
         *(uint32_t*)p = v;
-#endif
     } else {
         p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
     }
@@ -814,13 +784,9 @@ struct Des4T {
         }
         const uint32_t ue = __builtin_amdgcn_alignbit(te, te, se);
         const uint32_t uo = __builtin_amdgcn_alignbit(to, to, so);
-#ifdef TG_AB_DES_ANDOR
-        uint32_t v = lds_read32((ue & 0x1f80u) | be) ^ lds_read32((uo & 0x1f80u) | bo);
-#else
         // (u & 0x1f80) | base as an all-VGPR v_bitop3 (2 cycles) rather than v_and_or_b32 (4)
         uint32_t v = lds_read32(__builtin_amdgcn_bitop3_b32(ue, m, be, 0xEA)) ^
                      lds_read32(__builtin_amdgcn_bitop3_b32(uo, m, bo, 0xEA));
-#endif
         v ^= quad_dpp<0xB1>(v);
         v ^= quad_dpp<0x4E>(v);
         return v;

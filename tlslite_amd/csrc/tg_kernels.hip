@@ -1,6 +1,5 @@
 // tg_kernels.hip -- gfx950 kernels of libtlsgpu.so and their launchers:
 //   prefix/mac/cbc_kernel, tdes4_kernel   split AES / 3DES seal (tg_aes3.h)
-//   lseal_kernel     (A/B build TG_AB_LANE_SEAL only) AES seal with one lane per chain (tg_lane.h)
 //   rc4_seal_kernel  fused per-record MAC -> RC4 -> header, one lane per connection
 //                    chain (tlsrecordlayer.py:538-617, python_rc4.py:25-41)
 //   open_*_kernel    AES / 3DES open, block-parallel (tg_open3.h); rc4_open_kernel: RC4 open, lane per chain
@@ -623,11 +622,7 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
         hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire, pt,
                            states, meta, epoch);
     } else {
-#ifdef TG_AB_OPEN_QUAD
-        auto dec = open_dec_kernel<NR == 0 ? 10 : NR>;
-#else
         auto dec = open_aes_kernel<NR == 0 ? 10 : NR>;
-#endif
         if ((e = set_lds(dec, AES_DEC_LDS_BYTES)) != hipSuccess) return e;
         uint32_t grid = (nrecords + (O3_THREADS / 64) - 1) / (O3_THREADS / 64);
         grid = grid > cu_count() ? cu_count() : (grid ? grid : 1u);

@@ -9,13 +9,10 @@
 //   open_prefix_kernel  one lane per chain: length checks (:964-977), the
 //                       predecessor ciphertext block of every record's first
 //                       block, the connection's new residue.
-//   open_dec_kernel     16 waves per CU, 4 lanes per block (AES state column per
-//                       lane, DPP quad exchange), two blocks per quad; waves
-//                       walk records, 32 blocks of one record per step --
-//                       every block of every record in parallel.
 //   open_aes_kernel /   the decrypt with one lane per block (16 / 8 bytes), 64
-//   open_tdes_kernel    blocks of one record per wave step (round 2; the quad
-//                       open_dec_kernel is the A/B build TG_AB_OPEN_QUAD).
+//   open_tdes_kernel    blocks of one record per wave step -- every block of every
+//                       record in parallel (round 2; round 1's 4-lanes-per-block
+//                       open_dec_kernel measured slower and was removed in round 3).
 //   open_seq_kernel     one lane per chain: padding check (:979-993) on the
 //                       decrypted tail, which decides whether the MAC is
 //                       computed and so whether a seqnum is consumed (:1018).
@@ -47,9 +44,9 @@ static_assert(sizeof(OpenMeta) == 48, "OpenMeta");
 constexpr uint32_t OM_DEC = 1, OM_VERIFY = 2, OM_PADOK = 4;
 constexpr int O3_THREADS = 1024;
 
-// Equivalent inverse cipher on the quad layout (FIPS-197 5.3.5, rijndael.py:321-362):
-// column q of the next state = Td0[b0(q)] ^ Td1[b1(q-1)] ^ Td2[b2(q-2)] ^ Td3[b3(q-3)] ^ dk[q];
-// lane q's byte-b lookup feeds column q+b, i.e. lane i takes its term b from lane i-b.
+// LDS addressing of the equivalent-inverse-cipher tables (FIPS-197 5.3.5,
+// rijndael.py:321-362): the Td tables in the encryption tables' layout (aes_lds_fill with
+// dec = true) plus the 32-copy inverse S-box for the last round (lane_aes_dec).
 struct QuadAesDec {
     QuadAes t;  // same LDS addressing as the encryption tables (decrypt fill)
     uint32_t isb_base;
@@ -57,47 +54,10 @@ struct QuadAesDec {
         t.init();
         isb_base = 131072u + (__lane_id() & 31) * 4;
     }
-    // lane i reads lane i-1 / i-2 within the quad
-    template <int R>
-    __device__ __forceinline__ uint32_t round(uint32_t x, uint32_t k2) const {
-        const uint32_t t2 = t.look<2, 2>(x);
-        const uint32_t t3 = t.look<3, 3>(x);
-        const uint32_t t0 = t.look<0, 0>(x);
-        const uint32_t t1 = t.look<1, 1>(x);
-        const uint32_t u = (t2 ^ k2) ^ quad_dpp<0x93>(t3);
-        const uint32_t z = t0 ^ quad_dpp<0x93>(t1);
-        return z ^ quad_dpp<0x4E>(u);
-    }
     template <int B>
     __device__ __forceinline__ uint32_t isb(uint32_t x) const {  // InvS[byte B of x] << 8B
         const uint32_t idx = __builtin_amdgcn_ubfe(x, 8 * B, 8);
         return lds_read32(idx * 128u + isb_base) << (8 * B);
-    }
-    __device__ __forceinline__ uint32_t last(uint32_t x, uint32_t k2) const {
-        const uint32_t s2 = isb<2>(x);
-        const uint32_t s3 = isb<3>(x);
-        const uint32_t s0 = isb<0>(x);
-        const uint32_t s1 = isb<1>(x);
-        const uint32_t u = (s2 ^ k2) ^ quad_dpp<0x93>(s3);
-        const uint32_t z = s0 ^ quad_dpp<0x93>(s1);
-        return z ^ quad_dpp<0x4E>(u);
-    }
-    // two independent blocks, interleaved round by round; k as QuadAes::round_keys on dk
-    template <int NR>
-    __device__ __forceinline__ void decrypt2(uint32_t& a, uint32_t& b, const uint32_t* k) const {
-        a ^= k[0];
-        b ^= k[0];
-#pragma unroll
-        for (int r = 1; r < NR; r++) {
-            const uint32_t na = round<0>(a, k[r]);
-            const uint32_t nb = round<0>(b, k[r]);
-            a = na;
-            b = nb;
-        }
-        const uint32_t la = last(a, k[NR]);
-        const uint32_t lb = last(b, k[NR]);
-        a = la;
-        b = lb;
     }
 };
 
@@ -154,45 +114,6 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
     if (ok) {
 #pragma unroll
         for (int i = 0; i < (int)BS / 4; i++) st->iv[i] = res[i];
-    }
-}
-
-template <int NR>
-__global__ void __launch_bounds__(O3_THREADS, 1)
-open_dec_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
-                uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
-                uint32_t epoch) {
-    aes_lds_fill(nullptr, true);
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t quad = lane >> 2, q = lane & 3;
-    const uint32_t nwaves = gridDim.x * (O3_THREADS / 64);
-    QuadAesDec aes;
-    aes.init();
-    for (uint32_t r = blockIdx.x * (O3_THREADS / 64) + (threadIdx.x >> 6); r < nrecords; r += nwaves) {
-        const OpenMeta& mt = meta[r];
-        if (mt.epoch != epoch || !(mt.flags & OM_DEC)) continue;
-        const ConnState* st = states + mt.state;
-        uint32_t k[NR + 1];
-        QuadAes::round_keys<NR>(st->dk, q, k);
-        const tlsgpu_open_record R = recs[r];
-        const uint32_t E = st->explicit_iv ? 16u : 0u;
-        const uint32_t nb = R.ct_len >> 4;
-        const uint8_t* C = wire + R.ct_off + 4 * q;
-        uint8_t* P = pt + R.pt_off + 4 * q;
-        const bool al = (((uintptr_t)(wire + R.ct_off) | (uintptr_t)(pt + R.pt_off)) & 3) == 0;
-        const uint32_t pq = mt.pred[q];
-        for (uint32_t b0 = 0; b0 < nb; b0 += 32) {
-            const uint32_t ba = b0 + quad, bb = b0 + 16 + quad;
-            const bool va = ba < nb, vb = bb < nb;
-            uint32_t ca = va ? ld32(C + 16 * ba, al) : 0u;
-            uint32_t cb = vb ? ld32(C + 16 * bb, al) : 0u;
-            const uint32_t pa = ba == 0 ? pq : (va ? ld32(C + 16 * (ba - 1), al) : 0u);
-            const uint32_t pb = vb ? ld32(C + 16 * (bb - 1), al) : 0u;
-            aes.decrypt2<NR>(ca, cb, k);
-            if (va && 16 * ba >= E) st32(P + 16 * ba - E, ca ^ pa, al);
-            if (vb && 16 * bb >= E) st32(P + 16 * bb - E, cb ^ pb, al);
-        }
     }
 }
 

@@ -46,13 +46,11 @@ struct QuadAes {
     }
     template <int T, int B>  // T_t[byte B of s]
     __device__ __forceinline__ uint32_t look(uint32_t s) const {
-#ifndef TG_AB_OLD_ADDR
         if constexpr (B == 1) {
             // byte 1 already sits at the row-index bits: (s & 0xff00) | base, one 2-cycle
             // v_bitop3 instead of a 4-cycle v_perm
             return lds_read32(__builtin_amdgcn_bitop3_b32(s, m8, T >= 2 ? hi : lo, 0xEA) + (T & 1) * 128);
         }
-#endif
         constexpr uint32_t sel = 0x0c000000u | (2u << 16) | ((4u + B) << 8) | 0u;
         return lds_read32(perm(s, T >= 2 ? hi : lo, sel) + (T & 1) * 128);
     }
