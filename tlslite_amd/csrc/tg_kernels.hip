@@ -351,6 +351,17 @@ static bool many_chains(uint32_t nchains) {
 #endif
 }
 
+// The AES cipher phase runs 2 lanes per chain (cbc_pair_kernel) when every CU gets at
+// least a full workgroup of chains (C3_CHAINS = 256: cfg2, cfg3), the quad layout
+// (cbc_kernel, latency form) with fewer (cfg4's 2-16 chains per CU).
+static bool pair_regime(uint32_t nchains) {
+#ifdef TG_AB_NO_PAIR
+    return false;
+#else
+    return nchains >= (uint32_t)C3_CHAINS * cu_count();
+#endif
+}
+
 // phase 1 (stream s1): meta memset + seqnum prefix + per-record MAC / tail / header.
 // NR 0 = 3DES (8-byte blocks)
 template <int NR, int MAC, bool SSL3>
@@ -376,7 +387,9 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
 #else
     const bool mac_many = NR != 0 && many_chains(nchains);
 #endif
-    // (many chains: two 128-VGPR MAC waves per SIMD fit beside the cipher waves)
+    // (many chains: two 128-VGPR MAC waves per SIMD fit beside the cipher waves; beside the
+    // two 88-VGPR pair waves the 168-VGPR kernel would fit two too -- measured the same on
+    // cfg3, profiles/r03/ab_mac.txt)
     if (mac_many)
         hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS, MAC_LB_MANY, MAC_PF_MANY>), grid, dim3(256), 0, s, recs, r1, pt,
                            wire, states, wire_len, meta, tails, epoch, r0);
@@ -384,17 +397,6 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
         hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS>), grid, dim3(256), 0, s, recs, r1, pt, wire, states, wire_len,
                            meta, tails, epoch, r0);
     return hipGetLastError();
-}
-
-// The AES cipher phase runs 2 lanes per chain (cbc_pair_kernel) when every CU gets at
-// least a full workgroup of chains (C3_CHAINS = 256: cfg2, cfg3), the quad layout
-// (cbc_kernel, latency form) with fewer (cfg4's 2-16 chains per CU).
-static bool pair_regime(uint32_t nchains) {
-#ifdef TG_AB_NO_PAIR
-    return false;
-#else
-    return nchains >= (uint32_t)C3_CHAINS * cu_count();
-#endif
 }
 
 // phase 2 (stream s2, after phase 1): CBC over [explicit IV | P blocks | tail]
