@@ -116,8 +116,6 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
 //   TG_AB_NO_MANY       no many-chains configuration (12 cipher waves + 128-VGPR MAC kernel, cfg3)
 //   TG_AB_WAVES_MANY    cipher waves per CU in the many-chains configuration (default 12)
-//   TG_AB_DES_OLD       tdes4_kernel on the 32-copy SP tables (v_alignbit + v_bitop3 per lookup)
-//                       instead of the byte-row tables (v_perm for the even lookups)
 //   TG_AB_NO_PAIR    cipher phase on the quad layout (cbc_kernel) in the throughput regimes too,
 //                    instead of 2 lanes per chain (cbc_pair_kernel)
 //   TG_AB_PAIR_G1 / TG_AB_PAIR_GM  the pair kernel's prefetch group (blocks) in the one-generation
@@ -721,130 +719,97 @@ cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const
 // chain.  The Feistel function is eight SP-box lookups, four indexed by the bytes of
 // w = r ^ k_even (tables 7,5,3,1) and four by the bytes of v = rotr4(r) ^ k_odd =
 // rotr4(r ^ rotl4(k_odd)) (tables 6,4,2,0) -- des_rounds().  Lane j of a chain's quad
-// does the two lookups of byte j (one from w, one from v: a rotate, a key XOR, a 6-bit
-// extract and one conflict-free LDS read each), XORs them, and two DPP XOR steps
-// (quad [1,0,3,2], quad [2,3,0,1]) sum the eight terms in every lane of the quad.  A
-// round's critical path is one lookup + three XORs.  Measured against one lookup per lane
-// on 8 lanes (three DPP steps) at cfg5's 128 chains per CU: 6.24 vs 7.25 ms for the
-// cipher alone (tools/des_layout_microbench.hip) -- half the lanes, the same LDS
-// lookups, one DPP step fewer per round.  (l, r) are replicated in the quad; lanes 0/1
-// store the two ciphertext words.  Up to 128 chains per 512-thread workgroup.  The MAC,
-// the tail slot and the header come from prefix_kernel / mac_kernel<.., 8> as for AES.
+// covers byte j of both: ONE lookup in a combined table (Des4C below) returns the XOR of
+// its even and odd SP terms, and two DPP XOR steps (quad [1,0,3,2], quad [2,3,0,1]) sum
+// the four lanes' terms in every lane of the quad.  A round's critical path: 3-input key
+// XOR -> rotate -> mask|base -> one LDS read -> two DPP XORs.  (4 lanes per chain with
+// two lookups each measured 6.24 vs 7.25 ms against 8 lanes with one, round 2,
+// tools/des_layout_microbench.hip.)  (l, r) are replicated in the quad; lanes 0/1 store
+// the two ciphertext words.  Up to 128 chains per 512-thread workgroup.  The MAC, the tail
+// slot and the header come from prefix_kernel / mac_kernel<.., 8> as for AES.
 constexpr int D4_THREADS = 512;
 constexpr int D4_CHAINS = D4_THREADS / 4;
 
-// Round 3 table layout for tdes4_kernel ("byte rows"): the even S-boxes' 6-bit index is
-// the low 6 bits of byte j of w = r ^ k_even (DesSP's rotated domain), so a table with one
-// row per BYTE value (the index replicated over the byte's two top bits) is addressed by
-// one v_perm (byte j of w -> address bits 8..15 | the lane's column) instead of v_alignbit +
-// v_bitop3.  Row stride 256 B = 8 tables x 8 lane copies x 4 B: table slot s (0..3: the
-// even-path tables 7,5,3,1 of lanes j = 0..3; 4..7: the odd-path tables 6,4,2,0), copy =
-// the chain's index in its half-wave, so the 32 lanes of a half-wave hit banks 8j + copy:
-// conflict-free.  The odd path's index (bits 8j+4..8j+9 of t = r ^ rotl4(k_odd)) is not
-// byte-aligned: v_alignbit puts it at bits 8..13 and a v_bitop3 masks it (rows 0..63).
-// 64 KiB, as the 32-copy layout.
-__device__ __forceinline__ void des_lds_fill_rows(uint32_t* lds) {
+// tdes4_kernel's tables (round 3, "combined"): lane j's even index (bits 8j..8j+5 of r ^ k_even) and odd index
+// (bits 8j+4..8j+9 of r ^ rotl4(k_odd)) both lie in the 10-bit window x = bits 8j..8j+9 of
+// t = r ^ Kc_j, where Kc_j takes k_even's bits on 8j..8j+5 and rotl4(k_odd)'s on 8j+6..8j+9.
+// The two window bits both indices share (8j+4, 8j+5) see different key bits; their
+// difference d (2 key bits per lane and round) selects one of four tables:
+//   C_j[d][x] = SP[7-2j][x & 63] ^ SP[6-2j][((x >> 4) & 63) ^ d]
+// so a lane does ONE lookup per round (address: v_alignbit + v_bitop3 with the round's
+// per-lane base j*16K + d*4K), and the eight-term f is that lookup + the two DPP XOR steps.
+// 4 lanes x 4 d x 1024 x 4 B = 64 KiB, one copy (a half-wave's 32 lookups hit random banks:
+// the kernel is latency-bound, a conflict adds a few cycles to one read).  Replaces round 2's
+// two lookups per lane (32-copy SP tables; round 3's byte-row tables for the even half):
+// cfg5 164.2 -> 193.9 GiB/s, tdes4 6.08 -> 5.15 ms (same-box A/B, profiles/r03/ab_des.txt).
+__device__ __forceinline__ void des_lds_fill_comb(uint32_t* lds) {
     for (uint32_t idx = threadIdx.x; idx < 16384; idx += blockDim.x) {
-        const uint32_t row = idx >> 6, slot = (idx >> 3) & 7;
-        const uint32_t K = slot < 4 ? 7 - 2 * slot : 6 - 2 * (slot - 4);
-        lds[idx] = c_des.sp[K][row & 63];
+        const uint32_t j = idx >> 12, d = (idx >> 10) & 3, x = idx & 1023;
+        lds[idx] = c_des.sp[7 - 2 * j][x & 63] ^ c_des.sp[6 - 2 * j][((x >> 4) & 63) ^ d];
     }
 }
-// ROWS: the byte-row table layout above (des_lds_fill_rows); else the 32-copy layout of
-// des_lds_fill (rows of 6-bit indices, v_alignbit + v_bitop3 per lookup)
-template <bool ROWS>
-struct Des4T {
-    uint32_t be, bo, se, so, m;  // ROWS: se = the v_perm selector of the even lookup
+struct Des4C {
+    uint32_t s, m;
     __device__ __forceinline__ void init() {
-        const uint32_t lane = __lane_id(), j = lane & 3;
-        if constexpr (ROWS) {
-            const uint32_t copy = (lane >> 2) & 7;
-            m = vconst(0x3f00u);
-            be = (j * 8 + copy) * 4;
-            bo = ((4 + j) * 8 + copy) * 4;
-            se = 0x0c0c0000u | ((4u + j) << 8);  // address byte 1 <- byte j of w, byte 0 <- be
-            so = (8 * j + 28u) & 31u;            // t bits 8j+4 .. 8j+9 -> bits 8..13
-            return;
-        }
-        m = vconst(0x1f80u);
-        be = (lane & 31) * 4 + (7 - 2 * j) * 8192;
-        bo = (lane & 31) * 4 + (6 - 2 * j) * 8192;
-        // rotate so that the lane's 6 index bits (bit 8j of w, bit 8j+4 of t_odd) land at bits 7..12
-        se = (8 * j + 25u) & 31u;
-        so = (8 * j + 29u) & 31u;
+        const uint32_t j = __lane_id() & 3;
+        s = (8 * j + 30) & 31;  // rotr by 8j - 2: window bit 8j -> address bit 2
+        m = vconst(0xffcu);
     }
-    // Feistel f of te = r ^ k_even, to = r ^ rotl4(k_odd), summed over the quad
-    __device__ __forceinline__ uint32_t f(uint32_t te, uint32_t to) const {
-        if constexpr (ROWS) {
-            const uint32_t uo = __builtin_amdgcn_alignbit(to, to, so);
-            uint32_t v = lds_read32(perm(te, be, se)) ^ lds_read32(__builtin_amdgcn_bitop3_b32(uo, m, bo, 0xEA));
-            v ^= quad_dpp<0xB1>(v);
-            v ^= quad_dpp<0x4E>(v);
-            return v;
-        }
-        const uint32_t ue = __builtin_amdgcn_alignbit(te, te, se);
-        const uint32_t uo = __builtin_amdgcn_alignbit(to, to, so);
-        // (u & 0x1f80) | base as an all-VGPR v_bitop3 (2 cycles) rather than v_and_or_b32 (4)
-        uint32_t v = lds_read32(__builtin_amdgcn_bitop3_b32(ue, m, be, 0xEA)) ^
-                     lds_read32(__builtin_amdgcn_bitop3_b32(uo, m, bo, 0xEA));
+    // round constants of lane j from the round's even and (unrotated) odd key words
+    static __device__ __forceinline__ void key(uint32_t ke, uint32_t ko, uint32_t j, uint32_t& kc, uint32_t& kb) {
+        const uint32_t ko4 = (ko << 4) | (ko >> 28);
+        const uint32_t sh = 8 * j, so = (8 * j + 6) & 31;
+        const uint32_t me = 63u << sh, mo = (15u << so) | (15u >> (32 - so));  // rotl(15, so)
+        kc = (ke & me) | (ko4 & mo);
+        kb = j * 16384u + (((ke ^ ko4) >> (sh + 4)) & 3u) * 4096u;
+    }
+    __device__ __forceinline__ uint32_t f(uint32_t t, uint32_t kb) const {
+        const uint32_t u = __builtin_amdgcn_alignbit(t, t, s);
+        uint32_t v = lds_read32(__builtin_amdgcn_bitop3_b32(u, m, kb, 0xEA));
         v ^= quad_dpp<0xB1>(v);
         v ^= quad_dpp<0x4E>(v);
         return v;
     }
-    // block as two big-endian words; ke/ko[16p + i] = even / pre-rotated odd key word of
-    // pass p, round i.  The next round's key XORs take l ^ f ^ k in one 3-input XOR each.
-    __device__ __forceinline__ void block(uint32_t& hi, uint32_t& lo, const uint32_t* ke, const uint32_t* ko) const {
+    // block as two big-endian words; kc/kb[16p + i] = the lane's Kc and table base of pass p,
+    // round i.  The next round's key XOR takes l ^ f ^ Kc in one 3-input XOR.
+    __device__ __forceinline__ void block(uint32_t& hi, uint32_t& lo, const uint32_t* kc, const uint32_t* kb) const {
         uint32_t l = hi, r = lo;
         des_ip(l, r);
-        uint32_t te = r ^ ke[0], to = r ^ ko[0];
+        uint32_t t = r ^ kc[0];
 #pragma unroll
         for (int g = 0; g < 48; g++) {
-            const uint32_t fv = f(te, to);
+            const uint32_t fv = f(t, kb[g]);
             const uint32_t rn = l ^ fv;
             if (g % 16 != 15) {
-                if (g + 1 < 48) {
-                    te = __builtin_amdgcn_bitop3_b32(l, fv, ke[g + 1], 0x96);
-                    to = __builtin_amdgcn_bitop3_b32(l, fv, ko[g + 1], 0x96);
-                }
+                if (g + 1 < 48) t = __builtin_amdgcn_bitop3_b32(l, fv, kc[g + 1], 0x96);
                 l = r;
                 r = rn;
-            } else {  // end of a DES pass: (l, r) = (R16, L16) feeds the next pass
+            } else {
                 l = rn;
-                if (g + 1 < 48) {
-                    te = r ^ ke[g + 1];
-                    to = r ^ ko[g + 1];
-                }
+                if (g + 1 < 48) t = r ^ kc[g + 1];
             }
         }
         des_fp(l, r);
         hi = l;
         lo = r;
     }
-    // CBC on LE words (TdesCbc::enc_block): c = E(p ^ iv), iv = c
     __device__ __forceinline__ void cbc(uint32_t d0, uint32_t d1, uint32_t& iv0, uint32_t& iv1,
-                                        const uint32_t* ke, const uint32_t* ko) const {
+                                        const uint32_t* kc, const uint32_t* kb) const {
         uint32_t hi = bswap32(d0 ^ iv0), lo = bswap32(d1 ^ iv1);
-        block(hi, lo, ke, ko);
+        block(hi, lo, kc, kb);
         iv0 = bswap32(hi);
         iv1 = bswap32(lo);
     }
 };
-using Des4 = Des4T<false>;
-#ifdef TG_AB_DES_OLD
-constexpr bool DES_ROWS = false;
-#else
-constexpr bool DES_ROWS = true;
-#endif
 
 __global__ void __launch_bounds__(D4_THREADS, 1)
 tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
              uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
              ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,
              uint32_t cpw, uint32_t epoch) {
-    // SP tables at LDS offset 0 (the kernel's only LDS), read back by absolute address (Des4::f)
+    // combined tables at LDS offset 0 (the kernel's only LDS), read back by absolute address (Des4C::f)
     extern __shared__ __attribute__((aligned(16))) uint32_t d4_lds[];
-    if constexpr (DES_ROWS) des_lds_fill_rows(d4_lds);
-    else des_lds_fill(d4_lds);
+    des_lds_fill_comb(d4_lds);
     __syncthreads();
     const uint32_t j = threadIdx.x & 3;
     const uint32_t local = threadIdx.x >> 2;
@@ -852,17 +817,15 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
     if (local >= cpw || cid >= nchains) return;  // the 4 lanes of a chain leave together
     const tlsgpu_chain ch = chains[cid];
     ConnState* st = states + ch.state;
-    Des4T<DES_ROWS> D;
+    Des4C D;
     D.init();
-    uint32_t ke[48], ko[48];
+    uint32_t kc[48], kb[48];  // per round: Kc_j and the lane's table base
 #pragma unroll
     for (int p = 0; p < 3; p++)
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             const int k = p == 1 ? 15 - i : i;  // EDE: the middle pass decrypts (keys backwards)
-            const uint32_t od = st->des[p][2 * k + 1];
-            ke[16 * p + i] = st->des[p][2 * k];
-            ko[16 * p + i] = (od << 4) | (od >> 28);
+            Des4C::key(st->des[p][2 * k], st->des[p][2 * k + 1], j, kc[16 * p + i], kb[16 * p + i]);
         }
     uint32_t iv0 = st->iv[0], iv1 = st->iv[1];
     const uint32_t f0 = st->fixed_iv[0], f1 = st->fixed_iv[1];
@@ -880,7 +843,7 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
         uint8_t* B = wire + R.wire_off + 5;
         const bool al = (((uintptr_t)P | (uintptr_t)B) & 3) == 0;
         if (E) {  // E_K(fixedIVBlock ^ residue) (tlsrecordlayer.py:594-595)
-            D.cbc(f0, f1, iv0, iv1, ke, ko);
+            D.cbc(f0, f1, iv0, iv1, kc, kb);
             if (j < 2) st32(B + 4 * j, j ? iv1 : iv0, al);
         }
         uint8_t* O = B + E;
@@ -891,7 +854,7 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
             const uint32_t bn = b + 1 < nb ? b + 1 : b;  // prefetch, clamped to the last block
             n0 = ld32(P + 8 * bn, al);
             n1 = ld32(P + 8 * bn + 4, al);
-            D.cbc(d0, d1, iv0, iv1, ke, ko);
+            D.cbc(d0, d1, iv0, iv1, kc, kb);
             if (j < 2) st32(O + 8 * b + 4 * j, j ? iv1 : iv0, al);
         }
         // tail blocks from the MAC kernel's slot
@@ -899,7 +862,7 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
         uint8_t* Ot = O + 8 * nb;
         const uint32_t T = mt.tail_len;
         for (uint32_t off = 0; off < T; off += 8) {
-            D.cbc(*(const uint32_t*)(slot + off), *(const uint32_t*)(slot + off + 4), iv0, iv1, ke, ko);
+            D.cbc(*(const uint32_t*)(slot + off), *(const uint32_t*)(slot + off + 4), iv0, iv1, kc, kb);
             if (j < 2) st32(Ot + off + 4 * j, j ? iv1 : iv0, al);
         }
     }

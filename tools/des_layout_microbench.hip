@@ -74,7 +74,70 @@ struct Des8 {
     }
 };
 
-// 4 lanes per chain: tdes4_kernel's Des4 (tg_aes3.h).  2 and 1 lanes per chain: DesG,
+// Round 2's tdes4_kernel round (two lookups per lane on the 32-copy SP tables, des_lds_fill);
+// the product kernel moved to one lookup per lane on combined tables in round 3 (Des4C, tg_aes3.h).
+struct Des4 {
+    uint32_t be, bo, se, so, m;
+    __device__ __forceinline__ void init() {
+        const uint32_t lane = __lane_id(), j = lane & 3;
+        m = vconst(0x1f80u);
+        be = (lane & 31) * 4 + (7 - 2 * j) * 8192;
+        bo = (lane & 31) * 4 + (6 - 2 * j) * 8192;
+        // rotate so that the lane's 6 index bits (bit 8j of w, bit 8j+4 of t_odd) land at bits 7..12
+        se = (8 * j + 25u) & 31u;
+        so = (8 * j + 29u) & 31u;
+    }
+    // Feistel f of te = r ^ k_even, to = r ^ rotl4(k_odd), summed over the quad
+    __device__ __forceinline__ uint32_t f(uint32_t te, uint32_t to) const {
+        const uint32_t ue = __builtin_amdgcn_alignbit(te, te, se);
+        const uint32_t uo = __builtin_amdgcn_alignbit(to, to, so);
+        // (u & 0x1f80) | base as an all-VGPR v_bitop3 (2 cycles) rather than v_and_or_b32 (4)
+        uint32_t v = lds_read32(__builtin_amdgcn_bitop3_b32(ue, m, be, 0xEA)) ^
+                     lds_read32(__builtin_amdgcn_bitop3_b32(uo, m, bo, 0xEA));
+        v ^= quad_dpp<0xB1>(v);
+        v ^= quad_dpp<0x4E>(v);
+        return v;
+    }
+    // block as two big-endian words; ke/ko[16p + i] = even / pre-rotated odd key word of
+    // pass p, round i.  The next round's key XORs take l ^ f ^ k in one 3-input XOR each.
+    __device__ __forceinline__ void block(uint32_t& hi, uint32_t& lo, const uint32_t* ke, const uint32_t* ko) const {
+        uint32_t l = hi, r = lo;
+        des_ip(l, r);
+        uint32_t te = r ^ ke[0], to = r ^ ko[0];
+#pragma unroll
+        for (int g = 0; g < 48; g++) {
+            const uint32_t fv = f(te, to);
+            const uint32_t rn = l ^ fv;
+            if (g % 16 != 15) {
+                if (g + 1 < 48) {
+                    te = __builtin_amdgcn_bitop3_b32(l, fv, ke[g + 1], 0x96);
+                    to = __builtin_amdgcn_bitop3_b32(l, fv, ko[g + 1], 0x96);
+                }
+                l = r;
+                r = rn;
+            } else {  // end of a DES pass: (l, r) = (R16, L16) feeds the next pass
+                l = rn;
+                if (g + 1 < 48) {
+                    te = r ^ ke[g + 1];
+                    to = r ^ ko[g + 1];
+                }
+            }
+        }
+        des_fp(l, r);
+        hi = l;
+        lo = r;
+    }
+    // CBC on LE words (TdesCbc::enc_block): c = E(p ^ iv), iv = c
+    __device__ __forceinline__ void cbc(uint32_t d0, uint32_t d1, uint32_t& iv0, uint32_t& iv1,
+                                        const uint32_t* ke, const uint32_t* ko) const {
+        uint32_t hi = bswap32(d0 ^ iv0), lo = bswap32(d1 ^ iv1);
+        block(hi, lo, ke, ko);
+        iv0 = bswap32(hi);
+        iv1 = bswap32(lo);
+    }
+};
+
+// 4 lanes per chain: Des4 above.  2 and 1 lanes per chain: DesG,
 // lane j does the 8/LPC lookups of bytes [4j/LPC, 4(j+1)/LPC) of w and v.
 template <int LPC>
 struct DesG {
