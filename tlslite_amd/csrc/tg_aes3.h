@@ -737,14 +737,20 @@ constexpr int D4_CHAINS = D4_THREADS / 4;
 // difference d (2 key bits per lane and round) selects one of four tables:
 //   C_j[d][x] = SP[7-2j][x & 63] ^ SP[6-2j][((x >> 4) & 63) ^ d]
 // so a lane does ONE lookup per round (address: v_alignbit + v_bitop3 with the round's
-// per-lane base j*16K + d*4K), and the eight-term f is that lookup + the two DPP XOR steps.
-// 4 lanes x 4 d x 1024 x 4 B = 64 KiB, one copy (a half-wave's 32 lookups hit random banks:
-// the kernel is latency-bound, a conflict adds a few cycles to one read).  Replaces round 2's
+// per-lane base j*4 + d*16K), and the eight-term f is that lookup + the two DPP XOR steps.
+// 4 lanes x 4 d x 1024 x 4 B = 64 KiB, one copy (the 10-bit windows are random: bank
+// conflicts, PMC 0.7 of the LDS cycles; the kernel is latency-bound and a conflict adds a
+// few cycles to one read).  Replaces round 2's
 // two lookups per lane (32-copy SP tables; round 3's byte-row tables for the even half):
 // cfg5 164.2 -> 193.9 GiB/s, tdes4 6.08 -> 5.15 ms (same-box A/B, profiles/r03/ab_des.txt).
+// Layout: lane j's index bits sit in the address's bank bits (dword j + 4x + 4096d), so only
+// lanes of one j can collide: a half-wave's 8 lanes of each j share 8 banks instead of all 32
+// lanes sharing 32 (cfg5 5.147 -> 5.105 ms; a second copy in bank bit 4, 128 KiB: 5.86 ms;
+// profiles/r03/ab_des.txt).
+constexpr uint32_t D4_LDS_BYTES = 65536u;
 __device__ __forceinline__ void des_lds_fill_comb(uint32_t* lds) {
-    for (uint32_t idx = threadIdx.x; idx < 16384; idx += blockDim.x) {
-        const uint32_t j = idx >> 12, d = (idx >> 10) & 3, x = idx & 1023;
+    for (uint32_t idx = threadIdx.x; idx < D4_LDS_BYTES / 4; idx += blockDim.x) {
+        const uint32_t j = idx & 3, x = (idx >> 2) & 1023, d = idx >> 12;
         lds[idx] = c_des.sp[7 - 2 * j][x & 63] ^ c_des.sp[6 - 2 * j][((x >> 4) & 63) ^ d];
     }
 }
@@ -752,8 +758,8 @@ struct Des4C {
     uint32_t s, m;
     __device__ __forceinline__ void init() {
         const uint32_t j = __lane_id() & 3;
-        s = (8 * j + 30) & 31;  // rotr by 8j - 2: window bit 8j -> address bit 2
-        m = vconst(0xffcu);
+        s = (8 * j + 28) & 31;  // rotr by 8j - 4: window bit 8j -> address bit 4
+        m = vconst(0x3ff0u);
     }
     // round constants of lane j from the round's even and (unrotated) odd key words
     static __device__ __forceinline__ void key(uint32_t ke, uint32_t ko, uint32_t j, uint32_t& kc, uint32_t& kb) {
@@ -761,7 +767,7 @@ struct Des4C {
         const uint32_t sh = 8 * j, so = (8 * j + 6) & 31;
         const uint32_t me = 63u << sh, mo = (15u << so) | (15u >> (32 - so));  // rotl(15, so)
         kc = (ke & me) | (ko4 & mo);
-        kb = j * 16384u + (((ke ^ ko4) >> (sh + 4)) & 3u) * 4096u;
+        kb = j * 4u + (((ke ^ ko4) >> (sh + 4)) & 3u) * 16384u;
     }
     __device__ __forceinline__ uint32_t f(uint32_t t, uint32_t kb) const {
         const uint32_t u = __builtin_amdgcn_alignbit(t, t, s);

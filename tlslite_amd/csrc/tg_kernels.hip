@@ -410,9 +410,9 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
     if constexpr (NR == 0) {  // 3DES: 4 lanes per chain
         uint32_t pw = (nchains + ncu - 1) / ncu;
         pw = pw < 1 ? 1 : (pw > (uint32_t)D4_CHAINS ? (uint32_t)D4_CHAINS : pw);
-        hipError_t e = set_lds(tdes4_kernel, DES_LDS_BYTES);
+        hipError_t e = set_lds(tdes4_kernel, D4_LDS_BYTES);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(tdes4_kernel, dim3((nchains + pw - 1) / pw), dim3(D4_THREADS), DES_LDS_BYTES, s, chains,
+        hipLaunchKernelGGL(tdes4_kernel, dim3((nchains + pw - 1) / pw), dim3(D4_THREADS), D4_LDS_BYTES, s, chains,
                            nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch);
         return hipGetLastError();
     } else {
