@@ -721,8 +721,9 @@ cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const
 // rotr4(r ^ rotl4(k_odd)) (tables 6,4,2,0) -- des_rounds().  Lane j of a chain's quad
 // covers byte j of both: ONE lookup in a combined table (Des4C below) returns the XOR of
 // its even and odd SP terms, and two DPP XOR steps (quad [1,0,3,2], quad [2,3,0,1]) sum
-// the four lanes' terms in every lane of the quad.  A round's critical path: 3-input key
-// XOR -> rotate -> mask|base -> one LDS read -> two DPP XORs.  (4 lanes per chain with
+// the four lanes' terms in every lane of the quad.  A round's critical path: one LDS read
+// -> two DPP XORs -> rotate f into the lane's frame -> one v_bitop3 (the key and table-base
+// part of the next address is formed before f returns).  (4 lanes per chain with
 // two lookups each measured 6.24 vs 7.25 ms against 8 lanes with one, round 2,
 // tools/des_layout_microbench.hip.)  (l, r) are replicated in the quad; lanes 0/1 store
 // the two ciphertext words.  Up to 128 chains per 512-thread workgroup.  The MAC, the tail
@@ -769,40 +770,51 @@ struct Des4C {
         kc = (ke & me) | (ko4 & mo);
         kb = j * 4u + (((ke ^ ko4) >> (sh + 4)) & 3u) * 16384u;
     }
-    __device__ __forceinline__ uint32_t f(uint32_t t, uint32_t kb) const {
-        const uint32_t u = __builtin_amdgcn_alignbit(t, t, s);
-        uint32_t v = lds_read32(__builtin_amdgcn_bitop3_b32(u, m, kb, 0xEA));
-        v ^= quad_dpp<0xB1>(v);
-        v ^= quad_dpp<0x4E>(v);
-        return v;
+    // one round constant per lane and round: the round's address bits outside the window (its
+    // table base) and the key bits inside it, in the lane's rotated frame
+    static __device__ __forceinline__ uint32_t key2(uint32_t ke, uint32_t ko, uint32_t j) {
+        uint32_t kc, kb;
+        key(ke, ko, j, kc, kb);
+        const uint32_t s = (8 * j + 28) & 31;
+        return (((kc >> s) | (kc << (32 - s))) & 0x3ff0u) | kb;
     }
-    // block as two big-endian words; kc/kb[16p + i] = the lane's Kc and table base of pass p,
-    // round i.  The next round's key XOR takes l ^ f ^ Kc in one 3-input XOR.
-    __device__ __forceinline__ void block(uint32_t& hi, uint32_t& lo, const uint32_t* kc, const uint32_t* kb) const {
+    // 48 rounds in the lane's rotated frame (L, R) = (rotr(l, s), rotr(r, s)): the next
+    // round's address is x ^ (rotr(f, s) & m) with x = (L & m) ^ B2 formed before f returns,
+    // so after the last DPP XOR only the rotate of f and one v_bitop3 precede the next read
+    // (against a 3-input key XOR, the rotate and the mask before: cfg5 5.11 -> 5.00 ms)
+    __device__ __forceinline__ void block(uint32_t& hi, uint32_t& lo, const uint32_t* b2) const {
         uint32_t l = hi, r = lo;
         des_ip(l, r);
-        uint32_t t = r ^ kc[0];
+        uint32_t L = __builtin_amdgcn_alignbit(l, l, s), R = __builtin_amdgcn_alignbit(r, r, s);
+        uint32_t addr = __builtin_amdgcn_bitop3_b32(R, m, b2[0], 0x6A);  // (R & m) ^ b2
 #pragma unroll
         for (int g = 0; g < 48; g++) {
-            const uint32_t fv = f(t, kb[g]);
-            const uint32_t rn = l ^ fv;
+            uint32_t v = lds_read32(addr);
+            v ^= quad_dpp<0xB1>(v);
+            v ^= quad_dpp<0x4E>(v);
+            const uint32_t y = __builtin_amdgcn_alignbit(v, v, s);
+            const uint32_t rn = L ^ y;
             if (g % 16 != 15) {
-                if (g + 1 < 48) t = __builtin_amdgcn_bitop3_b32(l, fv, kc[g + 1], 0x96);
-                l = r;
-                r = rn;
-            } else {
-                l = rn;
-                if (g + 1 < 48) t = r ^ kc[g + 1];
+                if (g + 1 < 48)
+                    addr = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(L, m, b2[g + 1], 0x6A), y, m,
+                                                       0x78);  // x ^ (y & m)
+                L = R;
+                R = rn;
+            } else {  // end of a DES pass: (l, r) = (R16, L16) feeds the next pass
+                L = rn;
+                if (g + 1 < 48) addr = __builtin_amdgcn_bitop3_b32(R, m, b2[g + 1], 0x6A);
             }
         }
+        l = __builtin_amdgcn_alignbit(L, L, 32 - s);
+        r = __builtin_amdgcn_alignbit(R, R, 32 - s);
         des_fp(l, r);
         hi = l;
         lo = r;
     }
     __device__ __forceinline__ void cbc(uint32_t d0, uint32_t d1, uint32_t& iv0, uint32_t& iv1,
-                                        const uint32_t* kc, const uint32_t* kb) const {
+                                        const uint32_t* b2) const {
         uint32_t hi = bswap32(d0 ^ iv0), lo = bswap32(d1 ^ iv1);
-        block(hi, lo, kc, kb);
+        block(hi, lo, b2);
         iv0 = bswap32(hi);
         iv1 = bswap32(lo);
     }
@@ -825,13 +837,13 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
     ConnState* st = states + ch.state;
     Des4C D;
     D.init();
-    uint32_t kc[48], kb[48];  // per round: Kc_j and the lane's table base
+    uint32_t b2[48];  // per round: the lane's key / table-base word (Des4C::key2)
 #pragma unroll
     for (int p = 0; p < 3; p++)
 #pragma unroll
         for (int i = 0; i < 16; i++) {
             const int k = p == 1 ? 15 - i : i;  // EDE: the middle pass decrypts (keys backwards)
-            Des4C::key(st->des[p][2 * k], st->des[p][2 * k + 1], j, kc[16 * p + i], kb[16 * p + i]);
+            b2[16 * p + i] = Des4C::key2(st->des[p][2 * k], st->des[p][2 * k + 1], j);
         }
     uint32_t iv0 = st->iv[0], iv1 = st->iv[1];
     const uint32_t f0 = st->fixed_iv[0], f1 = st->fixed_iv[1];
@@ -849,7 +861,7 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
         uint8_t* B = wire + R.wire_off + 5;
         const bool al = (((uintptr_t)P | (uintptr_t)B) & 3) == 0;
         if (E) {  // E_K(fixedIVBlock ^ residue) (tlsrecordlayer.py:594-595)
-            D.cbc(f0, f1, iv0, iv1, kc, kb);
+            D.cbc(f0, f1, iv0, iv1, b2);
             if (j < 2) st32(B + 4 * j, j ? iv1 : iv0, al);
         }
         uint8_t* O = B + E;
@@ -860,7 +872,7 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
             const uint32_t bn = b + 1 < nb ? b + 1 : b;  // prefetch, clamped to the last block
             n0 = ld32(P + 8 * bn, al);
             n1 = ld32(P + 8 * bn + 4, al);
-            D.cbc(d0, d1, iv0, iv1, kc, kb);
+            D.cbc(d0, d1, iv0, iv1, b2);
             if (j < 2) st32(O + 8 * b + 4 * j, j ? iv1 : iv0, al);
         }
         // tail blocks from the MAC kernel's slot
@@ -868,7 +880,7 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
         uint8_t* Ot = O + 8 * nb;
         const uint32_t T = mt.tail_len;
         for (uint32_t off = 0; off < T; off += 8) {
-            D.cbc(*(const uint32_t*)(slot + off), *(const uint32_t*)(slot + off + 4), iv0, iv1, kc, kb);
+            D.cbc(*(const uint32_t*)(slot + off), *(const uint32_t*)(slot + off + 4), iv0, iv1, b2);
             if (j < 2) st32(Ot + off + 4 * j, j ? iv1 : iv0, al);
         }
     }
