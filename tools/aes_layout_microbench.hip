@@ -57,31 +57,7 @@ struct QuadAesB : QuadAes {
     }
 };
 
-// 2 lanes per chain: lane h holds columns a = 2h, b = 2h+1.  Column j of the next
-// state = T0[b0(s_j)] ^ T1[b1(s_j+1)] ^ T2[b2(s_j+2)] ^ T3[b3(s_j+3)] ^ k_j; each lane
-// XORs the two terms of its own columns and, with the partner's key column folded
-// in, the two terms the partner needs; one DPP swap per column joins them.
-struct PairAes : QuadAes {
-    __device__ __forceinline__ void round(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
-        const uint32_t a2 = look<2, 2>(a), b3 = look<3, 3>(b), a1 = look<1, 1>(a), b2 = look<2, 2>(b);
-        const uint32_t a0 = look<0, 0>(a), b1 = look<1, 1>(b), b0 = look<0, 0>(b), a3 = look<3, 3>(a);
-        const uint32_t sA = __builtin_amdgcn_bitop3_b32(a2, b3, ka, 0x96);
-        const uint32_t sB = __builtin_amdgcn_bitop3_b32(a1, b2, kb, 0x96);
-        a = (a0 ^ b1) ^ pair_dpp(sA);
-        b = (b0 ^ a3) ^ pair_dpp(sB);
-    }
-    // final round: S-box byte B of s sits at byte B of table (B+2)&3
-    __device__ __forceinline__ void last(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
-        const uint32_t ta0 = look<2, 0>(a), tb1 = look<3, 1>(b), ta2 = look<0, 2>(a), tb3 = look<1, 3>(b);
-        const uint32_t tb0 = look<2, 0>(b), ta3 = look<1, 3>(a), ta1 = look<3, 1>(a), tb2 = look<0, 2>(b);
-        const uint32_t oA = perm(tb1, ta0, 0x0c0c0500u);
-        const uint32_t sA = perm(tb3, ta2, 0x07020c0cu) ^ ka;
-        const uint32_t oB = perm(ta3, tb0, 0x070c0c00u);
-        const uint32_t sB = perm(tb2, ta1, 0x0c06010cu) ^ kb;
-        a = oA ^ pair_dpp(sA);
-        b = oB ^ pair_dpp(sB);
-    }
-};
+// 2 lanes per chain: the product's PairAes (tg_quad.h)
 
 __device__ __forceinline__ void lane_round(const QuadAes& L, uint32_t s[4], const uint32_t* k) {
     uint32_t t[4];
@@ -359,7 +335,14 @@ int main(int argc, char** argv) {
     c.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks, 2 * blocks));
     c.push_back(run<4, 1, 256>("quad1", d_ek, cus, blocks, blocks / 3));
     c.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks, blocks / 3));
-    const int bad = compare(a) | compare(b) | compare(c);
+    // many chains (cfg3: 4,096 per CU): one lane per chain at 12 / 16 waves, and at 8 waves
+    // beside the mac_kernel-shaped load
+    std::vector<Res> d;
+    d.push_back(run<1, 1, 512>("lane1", d_ek, cus, blocks, 2 * blocks));
+    d.push_back(run<2, 1, 512>("pair1", d_ek, cus, blocks, 2 * blocks));
+    run<1, 1, 768>("lane1", d_ek, cus, blocks);
+    run<1, 1, 1024>("lane1", d_ek, cus, blocks);
+    const int bad = compare(a) | compare(b) | compare(c) | compare(d);
     if (!bad) printf("all layouts agree\n");
     return bad;
 }
