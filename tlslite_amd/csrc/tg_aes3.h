@@ -615,12 +615,19 @@ __device__ __forceinline__ void pcbc_group(const PairAes& aes, const uint32_t* k
         for (int i = 0; i < PAIR_G; i++) f[i] = ld64t<AL>(Pn + 16 * i);
     }
     uint8_t* Ob = O + 16 * b0;
+    // the group's ciphertext is kept in registers and stored at the group's end: the chain's
+    // stores reach the L2 together and merge into whole lines (with aligned groups, pcbc_bulk)
+    uint2 o[PAIR_G];
 #pragma unroll
     for (int i = 0; i < PAIR_G; i++) {
         pair_block<NR>(aes, kw, ka, kb, va, vb, c[i].x, c[i].y);
-        st64t<AL>(Ob + 16 * i, va, vb);
+        o[i] = make_uint2(va, vb);
     }
+#pragma unroll
+    for (int i = 0; i < PAIR_G; i++) st64t<AL>(Ob + 16 * i, o[i].x, o[i].y);
 }
+
+constexpr uint32_t PAIR_ALIGN_MIN = 16;  // blocks: records this long align their groups
 
 template <int NR, int GI, bool AL>
 __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
@@ -628,24 +635,53 @@ __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw
                                           uint8_t* O, uint32_t nb) {
     if (nb == 0) return;
     constexpr uint32_t G = GI;
-    const uint32_t last = nb - 1;
-    uint2 f[G];
-#pragma unroll
-    for (int i = 0; i < (int)G; i++) f[i] = ld64t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
-    uint32_t b0 = 0;
-    if (nb >= 2 * G) {  // first group peeled, as cbc_bulk
-        pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, P, O, 0, last, f);
-        for (b0 = G; b0 + 2 * G <= nb; b0 += G) pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, P, O, b0, last, f);
+    // Records of at least PAIR_ALIGN_MIN blocks first run the head blocks up to the output's
+    // next (16 G)-byte boundary, so every group stores whole lines (G = 8) / sectors (G = 4).
+    // The head's loads and the first group's are issued together: one exposed load latency per
+    // record, as without the head (with the head's loads first, cfg3's 89-block records lost
+    // more than the alignment gained).  Same-box A/B against one store per block as it
+    // completed: cfg2 850-854 -> 908-911, cfg3 536-537 -> 551-553 GiB/s (profiles/r03/ab_pair.txt).
+    uint32_t head = 0;
+    if (nb >= PAIR_ALIGN_MIN) {
+        constexpr uint32_t A = 16 * G;
+        const uint32_t ob = (uint32_t)(uintptr_t)O & ~15u;  // the block address (lane offset dropped)
+        head = ((A - (ob & (A - 1))) & (A - 1)) >> 4;
+        head = head < nb ? head : nb;
     }
-    if (b0 + G <= nb) {
-        pcbc_group<NR, GI, AL, true>(aes, kw, ka, kb, va, vb, P, O, b0, last, f);
+    uint2 hp[G];
+#pragma unroll
+    for (int i = 0; i < (int)G; i++)
+        if ((uint32_t)i < head) hp[i] = ld64t<AL>(P + 16 * i);
+    const uint8_t* Pg = P + 16 * head;
+    uint8_t* Og = O + 16 * head;
+    const uint32_t ng = nb - head;
+    const uint32_t last = ng ? ng - 1 : 0;
+    uint2 f[G];
+    if (ng) {
+#pragma unroll
+        for (int i = 0; i < (int)G; i++) f[i] = ld64t<AL>(Pg + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
+    }
+#pragma unroll
+    for (int i = 0; i < (int)G; i++)
+        if ((uint32_t)i < head) {
+            pair_block<NR>(aes, kw, ka, kb, va, vb, hp[i].x, hp[i].y);
+            st64t<AL>(O + 16 * i, va, vb);
+        }
+    if (ng == 0) return;
+    uint32_t b0 = 0;
+    if (ng >= 2 * G) {  // first group peeled, as cbc_bulk
+        pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, 0, last, f);
+        for (b0 = G; b0 + 2 * G <= ng; b0 += G) pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f);
+    }
+    if (b0 + G <= ng) {
+        pcbc_group<NR, GI, AL, true>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f);
         b0 += G;
     }
 #pragma unroll
     for (int i = 0; i < (int)G; i++) {
-        if (b0 + i < nb) {
+        if (b0 + i < ng) {
             pair_block<NR>(aes, kw, ka, kb, va, vb, f[i].x, f[i].y);
-            st64t<AL>(O + 16 * (b0 + i), va, vb);
+            st64t<AL>(Og + 16 * (b0 + i), va, vb);
         }
     }
 }
@@ -867,7 +903,35 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
         uint8_t* O = B + E;
         const uint32_t nb = n >> 3;
         uint32_t n0 = ld32(P, al), n1 = ld32(P + 4, al);
-        for (uint32_t b = 0; b < nb; b++) {
+        uint32_t b = 0;
+        // groups of 8 blocks: every lane of the quad holds each block's two ciphertext words;
+        // lane j keeps blocks 2j, 2j+1 of the group and stores their 16 bytes at the group's end
+        // (one 64-B piece per chain per group instead of 8 B per block as it completed: the
+        // L2 merges whole sectors; cfg5 199.8 -> 210.5 GiB/s, tdes4 5.00 -> 4.74 ms)
+        for (; b + 8 <= nb; b += 8) {
+            uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint32_t d0 = n0, d1 = n1;
+                const uint32_t bn = b + i + 1 < nb ? b + i + 1 : b + i;  // prefetch, clamped to the last block
+                n0 = ld32(P + 8 * bn, al);
+                n1 = ld32(P + 8 * bn + 4, al);
+                D.cbc(d0, d1, iv0, iv1, b2);
+                if (i & 1) {
+                    k2 = j == (uint32_t)(i >> 1) ? iv0 : k2;
+                    k3 = j == (uint32_t)(i >> 1) ? iv1 : k3;
+                } else {
+                    k0 = j == (uint32_t)(i >> 1) ? iv0 : k0;
+                    k1 = j == (uint32_t)(i >> 1) ? iv1 : k1;
+                }
+            }
+            uint8_t* Og = O + 8 * (b + 2 * j);
+            st32(Og, k0, al);
+            st32(Og + 4, k1, al);
+            st32(Og + 8, k2, al);
+            st32(Og + 12, k3, al);
+        }
+        for (; b < nb; b++) {
             const uint32_t d0 = n0, d1 = n1;
             const uint32_t bn = b + 1 < nb ? b + 1 : b;  // prefetch, clamped to the last block
             n0 = ld32(P + 8 * bn, al);
