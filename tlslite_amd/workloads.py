@@ -78,16 +78,26 @@ class Workload:
         pt_stride = np.array([_round_up(int(x), 16) for x in self.pt_len])
         wlen = np.array([self._wire_len(g, int(n)) for g, n in self._rec_groups()], dtype=np.int64)
         self.wire_len = wlen
-        wire_stride = np.array([_round_up(int(w), 16) for w in wlen])
         # offsets in slot order
         ps = pt_stride[order]
-        ws = wire_stride[order]
         pt_off_slot = np.concatenate([[0], np.cumsum(ps)[:-1]])
-        wire_off_slot = np.concatenate([[0], np.cumsum(ws)[:-1]]) + 11
+        # Wire slots, packed in slot order: each record's body after its explicit IV starts at
+        # the same offset modulo 128 B as its plaintext (pt_off is 16-aligned, so the body is
+        # too), so the cipher phase's groups, aligned to the output's lines, also load whole
+        # plaintext lines (tg_aes3.h pcbc_bulk).  A sender writev()s [wire_off, wire_off+5+C).
+        eiv = np.array([self._explicit_iv(g) for g, _ in self._rec_groups()], dtype=np.int64)[order]
+        wl_slot = wlen[order]
+        wire_off_slot = np.empty(r, dtype=np.int64)
+        cur = 16
+        for k in range(r):
+            target = (int(pt_off_slot[k]) - 5 - int(eiv[k])) % 128
+            wo = cur + ((target - cur) % 128)
+            wire_off_slot[k] = wo
+            cur = wo + int(wl_slot[k])
         self.pt_off = pt_off_slot[self.slot_of].astype(np.uint64)
         self.wire_off = wire_off_slot[self.slot_of].astype(np.uint64)
         self.pt_bytes = int(ps.sum())
-        self.wire_bytes = int(ws.sum()) + 16
+        self.wire_bytes = cur + 128
         self.plaintext_total = int(self.pt_len.sum())
         self.wire_total = int(wlen.sum())
         # position of each chain's plaintext in the splitmix stream: by default
@@ -122,6 +132,14 @@ class Workload:
         for gi, g in enumerate(self.groups):
             for _ in range(g.nconn * g.recs_per_conn):
                 yield g, g.pt_len
+
+    @staticmethod
+    def _explicit_iv(g):
+        """bytes of explicit IV before the body (TLS >= 1.1 block ciphers, tlsrecordlayer.py:594-595)"""
+        cipher = suite_primitives(g.suite)[0]
+        if cipher == "rc4":
+            return 0
+        return (8 if cipher == "3des" else 16) if g.version >= (3, 2) else 0
 
     @staticmethod
     def _wire_len(g, n):
