@@ -904,6 +904,17 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
         const uint32_t nb = n >> 3;
         uint32_t n0 = ld32(P, al), n1 = ld32(P + 4, al);
         uint32_t b = 0;
+        // head blocks up to the output's next 64-B sector, so every group stores whole sectors
+        uint32_t head = ((64u - ((uint32_t)(uintptr_t)O & 63u)) & 63u) >> 3;
+        head = head < nb ? head : nb;
+        for (; b < head; b++) {
+            const uint32_t d0 = n0, d1 = n1;
+            const uint32_t bn = b + 1 < nb ? b + 1 : b;  // prefetch, clamped to the last block
+            n0 = ld32(P + 8 * bn, al);
+            n1 = ld32(P + 8 * bn + 4, al);
+            D.cbc(d0, d1, iv0, iv1, b2);
+            if (j < 2) st32(O + 8 * b + 4 * j, j ? iv1 : iv0, al);
+        }
         // groups of 8 blocks: every lane of the quad holds each block's two ciphertext words;
         // lane j keeps blocks 2j, 2j+1 of the group and stores their 16 bytes at the group's end
         // (one 64-B piece per chain per group instead of 8 B per block as it completed: the
