@@ -273,8 +273,15 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
             for (int L = 0; L < 4; L++)
                 nxt[k][L] = make_uint4(nxt[k][L].y + c, nxt[k][L].z ^ c, nxt[k][L].w, nxt[k][L].x);
 #else
+            // the ring is reloaded as a whole after its last slot is transposed: a record's
+            // consecutive 64-B chunks (whole 128-B lines) are requested back to back rather than
+            // one compression apart (cfg2 901-902 -> 916-918 GiB/s with PF = 2)
+            if (k == PF - 1) {
 #pragma unroll
-            for (int L = 0; L < 4; L++) nxt[k][L] = ldg16(PL[L] + 64 * min(c + PF, NL[L]));
+                for (int kk = 0; kk < PF; kk++)
+#pragma unroll
+                    for (int L = 0; L < 4; L++) nxt[kk][L] = ldg16(PL[L] + 64 * min(c0 + kk + PF, NL[L]));
+            }
 #endif
 #ifdef TG_AB_MAC_LOADONLY
             if (c < nfull) {

@@ -3,7 +3,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-O=gpurun_out/r03_pmcfinal
+O=gpurun_out/r03_pmcfinal4
 mkdir -p $O
 for c in cfg2 cfg3 cfg5; do
   bash tools/pmc_kernels.sh $c $O/pmc_$c > $O/pmc_$c.log 2>&1 || { echo "pmc $c failed"; tail -20 $O/pmc_$c.log; exit 1; }
