@@ -49,7 +49,13 @@ constexpr int C3_CHAINS = 16 * TG_AB_CBC_WAVES;
 #define TG_AB_WAVES_MANY 12
 #endif
 constexpr int C3_WAVES_MANY = TG_AB_WAVES_MANY;
-constexpr int MAC_LB_MANY = 4, MAC_PF_MANY = 1;
+#ifndef TG_AB_MAC_LB_MANY
+#define TG_AB_MAC_LB_MANY 4
+#endif
+#ifndef TG_AB_MAC_PF_MANY
+#define TG_AB_MAC_PF_MANY 1
+#endif
+constexpr int MAC_LB_MANY = TG_AB_MAC_LB_MANY, MAC_PF_MANY = TG_AB_MAC_PF_MANY;
 
 template <int CIPHER_ID, int MAC, bool SSL3>
 __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
@@ -116,6 +122,7 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
 //   TG_AB_NO_MANY       no many-chains configuration (12 cipher waves + 128-VGPR MAC kernel, cfg3)
 //   TG_AB_WAVES_MANY    cipher waves per CU in the many-chains configuration (default 12)
+//   TG_AB_MAC_LB_MANY / TG_AB_MAC_PF_MANY  launch bound / prefetch ring of the many-chains MAC kernel
 //   TG_AB_NO_PAIR    cipher phase on the quad layout (cbc_kernel) in the throughput regimes too,
 //                    instead of 2 lanes per chain (cbc_pair_kernel)
 //   TG_AB_PAIR_G1 / TG_AB_PAIR_GM  the pair kernel's prefetch group (blocks) in the one-generation
