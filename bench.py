@@ -37,8 +37,11 @@ GIB = float(1 << 30)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    # defaults: 500 + 500 steps (~1 s of GPU time for cfg2): under sustained load the GPU's clocks settle
+    # ~4 % above what a 5-step warmup + 50-step run sees (tools/r03/gpu_warm.sh); cfg4 (~0.12 s per
+    # step): 2 + 10.  Explicit --steps / --warmup are used as given.
+    ap.add_argument("--steps", type=int, default=None)
+    ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
     ap.add_argument("--records", type=int, default=None, help="override record count (debug)")
     ap.add_argument("--no-cpu", action="store_true", help="skip cpu_baseline")
@@ -51,7 +54,12 @@ def parse():
     ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="minimum CPU time of the cpu_baseline sample (the full batch, repeated)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 10 if a.config == "cfg4" else 500
+    if a.warmup is None:
+        a.warmup = 2 if a.config == "cfg4" else 500
+    return a
 
 
 # The reference's own pure-Python path (measured in the survey container through

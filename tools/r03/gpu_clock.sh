@@ -3,7 +3,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-O=gpurun_out/r03_clock
+O=gpurun_out/r03_clock2
 mkdir -p $O
 (timeout 20 rocm-smi --showclocks > $O/smi_probe.txt 2>&1; true)
 for v in base noload nomac; do
