@@ -537,10 +537,13 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
     for (uint32_t j = 0; j < ch.count; j++) {
         const uint32_t r = ch.first + j;
         if (r >= nrecords) break;
+        // the record descriptor is loaded with the meta entry, not behind its test (one memory
+        // latency fewer at each record's start)
+        const tlsgpu_record R = recs[r];
         const RecMeta mt = meta[r];
+        asm volatile("" ::"v"(R.pt_off), "v"(R.wire_off), "v"(R.pt_len));
         if (mt.epoch != epoch || mt.status != 1) continue;
         any = true;
-        const tlsgpu_record R = recs[r];
         const uint32_t n = R.pt_len;
         const uint8_t* P = pt + R.pt_off + 4 * q;
         uint8_t* B = wire + R.wire_off + 5;
@@ -736,10 +739,13 @@ cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const
         for (uint32_t j = 0; j < ch.count; j++) {
             const uint32_t r = ch.first + j;
             if (r >= nrecords) break;
+            // the record descriptor is loaded with the meta entry, not behind its test (one memory
+            // latency fewer at each record's start)
+            const tlsgpu_record R = recs[r];
             const RecMeta mt = meta[r];
+            asm volatile("" ::"v"(R.pt_off), "v"(R.wire_off), "v"(R.pt_len));
             if (mt.epoch != epoch || mt.status != 1) continue;
             any = true;
-            const tlsgpu_record R = recs[r];
             const uint32_t n = R.pt_len;
             const uint8_t* P = pt + R.pt_off + 8 * h;
             uint8_t* B = wire + R.wire_off + 5;
@@ -910,10 +916,13 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
     for (uint32_t q = 0; q < ch.count; q++) {
         const uint32_t r = ch.first + q;
         if (r >= nrecords) break;
+        // the record descriptor is loaded with the meta entry, not behind its test (one memory
+        // latency fewer at each record's start)
+        const tlsgpu_record R = recs[r];
         const RecMeta mt = meta[r];
+        asm volatile("" ::"v"(R.pt_off), "v"(R.wire_off), "v"(R.pt_len));
         if (mt.epoch != epoch || mt.status != 1) continue;
         any = true;
-        const tlsgpu_record R = recs[r];
         const uint32_t n = R.pt_len;
         const uint8_t* P = pt + R.pt_off;
         uint8_t* B = wire + R.wire_off + 5;
