@@ -71,10 +71,12 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
     ConnState* st = states + ch.state;
-    const bool ok = st->cipher == (uint32_t)CIPHER_ID && st->mac == (uint32_t)MAC &&
-                    st->ssl3 == (SSL3 ? 1u : 0u) && !st->raw;
+    // state header without short-circuit branches (one memory latency, as prefix_kernel)
+    const uint4 h0 = *(const uint4*)st;                         // cipher, mac, vmaj..maclen, ssl3
+    const uint4 h1 = *(const uint4*)((const uint8_t*)st + 16);  // seqnum (lo, hi), explicit_iv, raw
+    const bool ok = (h0.x == (uint32_t)CIPHER_ID) & (h0.y == (uint32_t)MAC) & (h0.w == (SSL3 ? 1u : 0u)) & (h1.w == 0u);
     constexpr uint32_t BS = CIPHER_ID == TLSGPU_CIPHER_3DES ? 8u : 16u;
-    const uint32_t E = st->explicit_iv ? BS : 0u;
+    const uint32_t E = h1.z ? BS : 0u;
     uint32_t res[4] = {st->iv[0], st->iv[1], BS == 16 ? st->iv[2] : 0u, BS == 16 ? st->iv[3] : 0u};
     for (uint32_t k = 0; k < ch.count; k++) {
         const uint32_t r = ch.first + k;
