@@ -99,6 +99,9 @@ def build_workload(name, rank, world, records=None):
         kw = {} if records is None else {"nconn": records}
         return W.cfg4(rank=rank, world=world, **kw)
     kw = {} if records is None else {"n": records}
+    if name == "cfg3":
+        # plaintext records on 128-B line boundaries (cfg2 / cfg5 records are 16 KiB: already)
+        kw["pt_align"] = int(os.environ.get("TLSGPU_BENCH_PT_ALIGN", "128"))
     return W.CONFIGS[name](**kw)
 
 

@@ -49,7 +49,8 @@ class Workload:
     array belongs to chain chain_of[r]; chains of one variant are launched
     together."""
 
-    def __init__(self, name, groups, seed, rec_order=None, chain_stream_start=None, rec_ctype=None, rec_flags=None):
+    def __init__(self, name, groups, seed, rec_order=None, chain_stream_start=None, rec_ctype=None, rec_flags=None,
+                 pt_align=16):
         self.name, self.groups, self.seed = name, groups, seed
         # flat records in chain order
         states, pt_len, chain_first, chain_count, chain_group = [], [], [], [], []
@@ -75,7 +76,10 @@ class Workload:
         order = np.arange(r) if rec_order is None else np.asarray(rec_order)
         self.slot_of = np.empty(r, dtype=np.int64)
         self.slot_of[order] = np.arange(r)
-        pt_stride = np.array([_round_up(int(x), 16) for x in self.pt_len])
+        # plaintext slots at pt_align-byte boundaries (16: packed; bench.py uses 128 so every record
+        # starts on a line: the MAC kernel's 64-B chunks then never straddle two lines)
+        self.pt_align = int(pt_align)
+        pt_stride = np.array([_round_up(int(x), self.pt_align) for x in self.pt_len])
         wlen = np.array([self._wire_len(g, int(n)) for g, n in self._rec_groups()], dtype=np.int64)
         self.wire_len = wlen
         # offsets in slot order
@@ -348,12 +352,13 @@ def cfg2(n=65536, pt_len=16384, seed=2):
                     [g], seed)
 
 
-def cfg3(n=1048576, pt_len=1434, seed=3):
+def cfg3(n=1048576, pt_len=1434, seed=3, pt_align=16):
     rng = np.random.default_rng(seed)
     key, mk, fiv = rng.bytes(32), rng.bytes(32), rng.bytes(16)
     ivs = np.frombuffer(rng.bytes(16 * n), dtype=np.uint8).reshape(n, 16)
     g = Group("AES256-SHA256", (3, 3), [key], ivs, [mk], [fiv], np.arange(n, dtype=np.uint64), 1, pt_len)
-    return Workload("cfg3: %d x %d B records, TLS_RSA_WITH_AES_256_CBC_SHA256, TLS 1.2" % (n, pt_len), [g], seed)
+    return Workload("cfg3: %d x %d B records, TLS_RSA_WITH_AES_256_CBC_SHA256, TLS 1.2" % (n, pt_len), [g], seed,
+                    pt_align=pt_align)
 
 
 def cfg4(nconn=4096, recs_per_conn=256, pt_len=16384, seed=4, rank=0, world=1):
