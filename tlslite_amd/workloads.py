@@ -357,8 +357,10 @@ def cfg3(n=1048576, pt_len=1434, seed=3, pt_align=16):
     key, mk, fiv = rng.bytes(32), rng.bytes(32), rng.bytes(16)
     ivs = np.frombuffer(rng.bytes(16 * n), dtype=np.uint8).reshape(n, 16)
     g = Group("AES256-SHA256", (3, 3), [key], ivs, [mk], [fiv], np.arange(n, dtype=np.uint64), 1, pt_len)
-    return Workload("cfg3: %d x %d B records, TLS_RSA_WITH_AES_256_CBC_SHA256, TLS 1.2" % (n, pt_len), [g], seed,
-                    pt_align=pt_align)
+    name = "cfg3: %d x %d B records, TLS_RSA_WITH_AES_256_CBC_SHA256, TLS 1.2" % (n, pt_len)
+    if pt_align != 16:
+        name += ", plaintext records %d-B aligned" % pt_align
+    return Workload(name, [g], seed, pt_align=pt_align)
 
 
 def cfg4(nconn=4096, recs_per_conn=256, pt_len=16384, seed=4, rank=0, world=1):
