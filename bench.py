@@ -5,6 +5,13 @@ TLS-record seal of 64 Ki x 16 KiB records (config 2), in plaintext GiB/s.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
+With --gpus N > 1 and no launcher environment (WORLD_SIZE unset) bench.py starts the N
+ranks itself: before any GPU call it spawns N child processes of itself with RANK =
+LOCAL_RANK = i, WORLD_SIZE = N and a rendezvous address, waits for them, and exits
+non-zero if any fails; rank 0 prints the line.  N above the visible devices is refused
+unless --share-devices is given (ranks then share GPUs round-robin: a rehearsal of the
+N-rank path on a smaller box, not a scaling measurement).
+
 A step = one seal of the whole per-GPU batch (every record MAC'd, padded,
 CBC-encrypted and framed; connection states carried from the previous step).
 Multi-GPU is weak scaling: each rank owns its own batch on its own device
@@ -12,7 +19,9 @@ Multi-GPU is weak scaling: each rank owns its own batch on its own device
 the start/stop barriers and the max-over-ranks time (tlslite_amd.shard: a small
 TCP rendezvous, no PyTorch).  After the timed loop the same number of seals is
 replayed sequentially from the initial states and the last step's wire arena,
-wire lengths and final states are compared (`timed_bit_exact`).
+wire lengths and final states are compared (`timed_bit_exact`: a pipeline-vs-sequential
+consistency check), and a sample of chains is sealed the same number of times by the CPU
+oracle and compared with the last step's output (`timed_oracle_exact`).
 
 Prints ONE JSON line (rank 0) with roofline + cpu_baseline objects.
 """
@@ -37,8 +46,16 @@ GIB = float(1 << 30)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--share-devices", action="store_true",
+                    help="allow --gpus N above the visible device count (ranks share GPUs round-robin)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank plumbing only (no GPU call): every rank reports its RANK / LOCAL_RANK / device, rank 0 "
+                         "prints one JSON line; TLSGPU_DRYRUN_DEVICES stands in for the visible device count")
+    ap.add_argument("--pt-align", type=int, default=16,
+                    help="plaintext slot alignment of the workload (16: packed, as generic callers lay records out; "
+                         "128: every record on a cache line)")
     # defaults: 500 + 500 steps (~1 s of GPU time for cfg2): under sustained load the GPU's clocks settle
-    # ~4 % above what a 5-step warmup + 50-step run sees (tools/r03/gpu_warm.sh); cfg4 (~0.12 s per
+    # ~4 % above what a 5-step warmup + 50-step run sees (profiles/r03/warmup_steps.txt); cfg4 (~0.12 s per
     # step): 2 + 10.  Explicit --steps / --warmup are used as given.
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
@@ -93,25 +110,22 @@ def usable_cpus():
     return n, ", ".join(note)
 
 
-def build_workload(name, rank, world, records=None):
+def build_workload(name, rank, world, records=None, pt_align=16):
     from tlslite_amd import workloads as W
     if name == "cfg4":
         kw = {} if records is None else {"nconn": records}
         return W.cfg4(rank=rank, world=world, **kw)
     kw = {} if records is None else {"n": records}
     if name == "cfg3":
-        # plaintext records on 128-B line boundaries (cfg2 / cfg5 records are 16 KiB: already)
-        kw["pt_align"] = int(os.environ.get("TLSGPU_BENCH_PT_ALIGN", "128"))
+        # packed 16-B plaintext slots by default; --pt-align 128 puts every record on a line
+        # (cfg2 / cfg5 records are 16 KiB: line-aligned either way)
+        kw["pt_align"] = int(pt_align)
     return W.CONFIGS[name](**kw)
 
 
-def oracle_check(wl, wire_gpu, nthreads, sample=None, min_seconds=0.0):
-    """Seal the same workload with the CPU oracle; returns (bit_exact, seconds,
-    records, plaintext bytes, threads, repetitions).  After the first (checked)
-    pass the batch is sealed again -- connection states carried on, as the GPU
-    steps do -- until min_seconds have been timed in total."""
+def oracle_protos(wl, idx_chains):
+    """CPU-oracle connection states (initial) of the workload's chains idx_chains."""
     from oracle import oracle as O
-    idx_chains = np.arange(wl.n_chains) if sample is None else sample
     protos = []
     for c in idx_chains:
         g = wl.groups[wl.chain_group[c]]
@@ -122,6 +136,44 @@ def oracle_check(wl, wire_gpu, nthreads, sample=None, min_seconds=0.0):
         iv = bytes(g.ivs[gi]) if g.ivs is not None else b""
         protos.append(O.Conn.for_suite(g.suite, g.version, bytes(key), iv, bytes(mk),
                                        None if fiv is None else bytes(fiv), int(g.seq0[gi])))
+    return protos
+
+
+def oracle_timed_check(wl, wire_last, len_last, n_launches, nthreads, budget_bytes=384 << 20):
+    """The last timed step's output against the CPU oracle on a sample of chains: each
+    sampled chain is sealed n_launches times in succession from its initial state (states
+    carried, as the GPU's successive steps carry them) and its records of the last pass
+    must equal the GPU's final wire arena and wire lengths.  The sample is spread over
+    the batch and sized to ~budget_bytes of oracle plaintext.  -> (ok, chains sampled)."""
+    from oracle import oracle as O
+    per_chain = np.array([int(wl.pt_len[int(wl.chain_first[c]):int(wl.chain_first[c] + wl.chain_count[c])].sum())
+                          for c in range(wl.n_chains)], dtype=np.int64)
+    avg = max(1, int(per_chain.mean()) * max(1, n_launches))
+    k = int(min(wl.n_chains, max(2, budget_bytes // avg), 256))
+    idx = np.unique(np.linspace(0, wl.n_chains - 1, k).astype(np.int64))
+    protos = oracle_protos(wl, idx)
+    pt = wl.host_plaintext(O.fill_pattern)
+    wire = np.zeros(wl.wire_bytes, dtype=np.uint8)
+    lens = None
+    for _ in range(n_launches):
+        lens = O.seal_batch(protos, wl.chain_first[idx], wl.chain_count[idx], pt, wl.pt_off, wl.pt_len, wire,
+                            wl.wire_off, nthreads=nthreads, update=True)
+    for c in idx:
+        for r in range(int(wl.chain_first[c]), int(wl.chain_first[c] + wl.chain_count[c])):
+            o, L = int(wl.wire_off[r]), int(wl.wire_len[r])
+            if int(lens[r]) != int(len_last[r]) or not np.array_equal(wire[o:o + L], wire_last[o:o + L]):
+                return False, len(idx)
+    return True, len(idx)
+
+
+def oracle_check(wl, wire_gpu, nthreads, sample=None, min_seconds=0.0):
+    """Seal the same workload with the CPU oracle; returns (bit_exact, seconds,
+    records, plaintext bytes, threads, repetitions).  After the first (checked)
+    pass the batch is sealed again -- connection states carried on, as the GPU
+    steps do -- until min_seconds have been timed in total."""
+    from oracle import oracle as O
+    idx_chains = np.arange(wl.n_chains) if sample is None else sample
+    protos = oracle_protos(wl, idx_chains)
     pt = wl.host_plaintext(O.fill_pattern)
     wire = np.zeros(wl.wire_bytes, dtype=np.uint8)
     t0 = time.perf_counter()
@@ -377,18 +429,98 @@ def copy_rate(wl, stream, reps=5):
     return 2.0 * n / (best / 1e3) / 1e9
 
 
+def probe_device_count():
+    """GPUs visible to libtlsgpu.so, counted in a child process so that this process
+    touches no GPU before it spawns the ranks."""
+    import subprocess
+    code = "import sys; sys.path.insert(0, %r); from tlslite_amd.device import device_count; print(device_count())" % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        raise SystemExit("bench.py: device probe failed: %s" % r.stderr[-2000:])
+    return int(r.stdout.strip().splitlines()[-1])
+
+
+def spawn_ranks(args):
+    """--gpus N > 1 without a launcher: one child process per rank (RANK = LOCAL_RANK = i,
+    WORLD_SIZE = N, a free rendezvous port on 127.0.0.1), started before this process
+    makes any GPU call.  Returns the exit code: non-zero if any rank fails (the others are
+    then terminated)."""
+    import socket
+    import subprocess
+    ndev = int(os.environ.get("TLSGPU_DRYRUN_DEVICES", args.gpus)) if args.dry_run else probe_device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible to libtlsgpu.so")
+    if args.gpus > ndev and not args.share_devices:
+        raise SystemExit("bench.py: --gpus %d but only %d GPU(s) visible; pass --share-devices to run %d ranks on "
+                         "them round-robin (a rehearsal, not a scaling measurement)" % (args.gpus, ndev, args.gpus))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    token = os.urandom(8).hex()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TLSGPU_RDZV_PORT=str(port), TLSGPU_RDZV_TOKEN=token)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    import time as _t
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print("bench.py: rank %d exited with %d; stopping the others" % (procs.index(p), code), file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        _t.sleep(0.05)
+    return rc
+
+
+def dry_run(args, D):
+    """--dry-run: the N-rank plumbing without the GPU (CPU tests of the spawner)."""
+    from tlslite_amd.shard import device_for_rank
+    ndev = int(os.environ.get("TLSGPU_DRYRUN_DEVICES", max(D.world, 1)))
+    if D.world > ndev and not args.share_devices:
+        raise SystemExit("bench.py: %d ranks but only %d GPU(s) visible" % (D.world, ndev))
+    if os.environ.get("TLSGPU_DRYRUN_FAIL_RANK") == str(D.rank):
+        sys.exit(3)
+    me = {"rank": D.rank, "local_rank": D.local, "device": device_for_rank(D.local, ndev), "pid": os.getpid()}
+    ranks = [json.loads(b) for b in D.gather_bytes(json.dumps(me).encode())]
+    t = D.max(0.001 * (1 + D.rank))
+    if D.rank == 0:
+        print(json.dumps({"metric": "dry-run", "n_gpus": D.world, "ranks": ranks, "t_max": t,
+                          "devices_shared": D.world > ndev}))
+    D.close()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     from tlslite_amd.shard import ShardGroup, device_for_rank
     D = ShardGroup()
+    if D.world != args.gpus:
+        print("bench.py: WORLD_SIZE %d from the launcher, --gpus %d: running %d ranks" % (D.world, args.gpus, D.world),
+              file=sys.stderr)
+    if args.dry_run:
+        return dry_run(args, D)
     from tlslite_amd import _native as N
     from tlslite_amd.device import Event, Stream, set_device, synchronize, device_count, arch
-    if device_count() < 1:
+    ndev = device_count()
+    if ndev < 1:
         raise SystemExit("bench.py: no GPU visible to libtlsgpu.so")
-    dev = device_for_rank(D.local, device_count())
+    if D.world > ndev and not args.share_devices and os.environ.get("TLSGPU_SHARE_DEVICES") != "1":
+        raise SystemExit("bench.py: %d ranks but only %d GPU(s) visible; pass --share-devices to share them "
+                         "round-robin (a rehearsal, not a scaling measurement)" % (D.world, ndev))
+    dev = device_for_rank(D.local, ndev)
     set_device(dev)
     dev_arch = arch(dev)
-    wl = build_workload(args.config, D.rank, D.world, args.records)
+    wl = build_workload(args.config, D.rank, D.world, args.records, args.pt_align)
     stream = Stream()
     wl.to_device(stream)
     stream.synchronize()
@@ -464,7 +596,8 @@ def main():
     # ---- the timed output itself: replay the same number of seals one call at a time
     # (tlsgpu_seal_dev, one stream) from the initial states; the last step's wire arena,
     # wire lengths and the final states must equal the pipelined / concurrent run's
-    timed_ok = None
+    timed_ok = timed_oracle = None
+    timed_oracle_chains = 0
     if not args.no_check:
         got = (wl.d_wire.download(), wl.d_len.download(), wl.d_states.download())
         wl.reset_states(stream)
@@ -473,8 +606,13 @@ def main():
         stream.synchronize()
         ok = (np.array_equal(got[0], wl.d_wire.download()) and np.array_equal(got[1], wl.d_len.download())
               and np.array_equal(got[2], wl.d_states.download()))
-        del got
         timed_ok = D.sum(0.0 if ok else 1.0) == 0.0
+        # ... and the last step's output against the CPU oracle on a sample of chains
+        oo, timed_oracle_chains = oracle_timed_check(wl, got[0], got[1].view(np.int32), n_state_launches,
+                                                     usable_cpus()[0])
+        del got
+        timed_oracle = D.sum(0.0 if oo else 1.0) == 0.0
+        timed_oracle_chains = int(D.sum(timed_oracle_chains))
     t_max = D.max(wall)
     total_pt = D.sum(wl.plaintext_total * args.steps)
     value = total_pt / GIB / t_max
@@ -503,7 +641,8 @@ def main():
     achieved = alg_bytes / (avg_ms / 1e3) / 1e9
     copy_gbs = copy_rate(wl, stream)
     # HBM bytes per launch of the same kernel from the committed PMC summary
-    # (tools/pmc_kernels.sh -> profiles/pmc_<cfg>.json), only when it names this kernel
+    # (tools/pmc_kernels.sh -> profiles/pmc_<cfg>.json), only when it names this kernel and
+    # was collected on this workload; otherwise traffic is null
     traffic = seal_call_bytes = None
     tpath = args.traffic or os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
     if os.path.exists(tpath):
@@ -513,13 +652,15 @@ def main():
             # same kernel as cbc_kernel<10, false>: the second argument is the round's form)
             def _key(k):
                 return (k or "").split(",")[0].rstrip(">")
-            if _key(pj.get("dominant_kernel")) == _key(wl.dominant_kernel()):
+            # ... and only when the PMC run sealed this very workload (name, record count)
+            if (_key(pj.get("dominant_kernel")) == _key(wl.dominant_kernel())
+                    and pj.get("workload") == wl.name and pj.get("records") == wl.n_records):
                 traffic = pj.get("hbm_bytes_per_launch")
                 seal_call_bytes = pj.get("seal_call_hbm_bytes")
         except Exception:
             traffic = seal_call_bytes = None
     state_bytes = wl.cipher_state_bytes()
-    lookups = wl.aes_lookups() if wl.dominant_kernel().startswith(("cbc_kernel", "cbc_pair_kernel")) else None
+    lookups = wl.aes_lookups() if wl.dominant_kernel().startswith(("cbc_kernel", "cbc_pair_kernel", "seal_fused_kernel")) else None
     lds = None
     if lookups:
         g = lookups / (avg_ms / 1e3) / 1e9
@@ -569,6 +710,7 @@ def main():
             "config": {"workload": wl.name, "records_per_gpu": wl.n_records,
                        "plaintext_bytes_per_gpu": wl.plaintext_total,
                        "parallelism": "connection-sharded x%d (no collective)" % D.world,
+                       "devices_shared": D.world > ndev,
                        "device": dev_arch},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -594,8 +736,13 @@ def main():
             "cpu_baseline": cpu,
             "bit_exact": bit_exact,
             "timed_bit_exact": timed_ok,
-            "timed_check": "the %d seals before the last step's output replayed one call at a time from the "
-                           "initial states: last wire arena, wire lengths and final states equal" % n_state_launches,
+            "timed_check": "pipeline-vs-sequential consistency: the %d seals before the last step's output "
+                           "replayed one tlsgpu_seal_dev call at a time from the initial states; last wire arena, "
+                           "wire lengths and final states equal the pipelined run's" % n_state_launches,
+            "timed_oracle_exact": timed_oracle,
+            "timed_oracle_check": "%d sampled chains sealed %d times in succession by the CPU oracle from their "
+                                  "initial states: their records equal the last timed step's wire arena and "
+                                  "wire lengths" % (timed_oracle_chains, n_state_launches),
             "host_inclusive": host_inc,
             "open": open_res,
             "derive": derive_res,

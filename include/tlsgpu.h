@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TLSGPU_ABI_VERSION 3
+#define TLSGPU_ABI_VERSION 4
 
 /* ---- suite components (tlsrecordlayer.py:1063-1095, constants.py:159-201) */
 enum {
@@ -185,6 +185,8 @@ int tlsgpu_memset(void *dptr, int value, size_t bytes, tlsgpu_stream s);
 
 /* ---- streams / events ---------------------------------------------------- */
 int tlsgpu_stream_create(tlsgpu_stream *s);
+/* waits for the stream, frees the library-owned seal / open workspaces of this stream
+ * (tlsgpu_seal_dev / tlsgpu_open_dev with a NULL workspace), then destroys it */
 int tlsgpu_stream_destroy(tlsgpu_stream s);
 int tlsgpu_stream_synchronize(tlsgpu_stream s);
 int tlsgpu_event_create(tlsgpu_event *e);
@@ -227,10 +229,13 @@ int tlsgpu_seal_wire_len(const tlsgpu_conn_state *st, uint32_t pt_len, uint32_t 
  * per (device, stream): calls on different streams never share one. */
 size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords);
 /* Free every library-owned seal / open workspace (the NULL-workspace buffers, one per
- * (device, stream) ever used).  Waits for each device they live on first.  Callers that
- * create and destroy many streams call it; otherwise the buffers live until exit.  Must
- * not run concurrently with a seal / open call that passes a NULL workspace. */
+ * (device, stream) in use; the device is the stream's).  Waits for each device they live
+ * on first; every entry is dropped even when a HIP call fails (the first error is
+ * returned).  tlsgpu_stream_destroy already frees its stream's buffers.  Must not run
+ * concurrently with a seal / open call that passes a NULL workspace. */
 int tlsgpu_release_workspaces(void);
+/* number of library-owned workspaces currently allocated (diagnostics / tests) */
+size_t tlsgpu_owned_workspace_count(void);
 /* Name of the cipher-phase kernel a seal call of `nchains` chains of `variant` runs on the
  * current device (its rocprofv3 name stem, e.g. "cbc_kernel<10, false>"): the layout is
  * chosen from the chains per CU.  Diagnostics / profiling only. */

@@ -451,29 +451,94 @@ def test_many_chains_vs_oracle(suite, version):
 
 
 def test_library_workspaces_released_and_reallocated():
-    """tlsgpu_seal_dev with a NULL workspace on several short-lived streams, then
-    tlsgpu_release_workspaces (which frees the library-owned buffers after waiting for the
-    device), then more NULL-workspace seals: every batch equals the first (no state of a
-    freed buffer leaks into a later call)."""
+    """tlsgpu_seal_dev with a NULL workspace on several short-lived streams: destroying a
+    stream frees the library-owned workspace of that stream (the count of owned buffers
+    drops back; a later stream that gets the same handle value starts without one), and
+    every batch equals the first (no state of a freed buffer leaks into a later call).
+    tlsgpu_release_workspaces then frees whatever is left (the null stream's buffer)."""
     _T()
     from tlslite_amd import _native as N
     from tlslite_amd import workloads as W
-    from tlslite_amd.device import Stream
+    from tlslite_amd.device import Stream, synchronize
     from tlslite_amd.recordlayer import seal_dev
     wl = W.cfg2(n=300, pt_len=3001, seed=31)
     wl.to_device()
     var, d_ch, nch = wl.launches[0]
+    N.call("tlsgpu_release_workspaces")
+    assert N.lib.tlsgpu_owned_workspace_count() == 0
     outs = []
     for k in range(6):
         s = Stream()
         wl.reset_states(s)
         wl.d_wire.zero(s)
         seal_dev(d_ch, nch, wl.d_recs, wl.n_records, wl.d_pt, wl.d_wire, wl.d_states, wl.d_len, var, None, s)
+        assert N.lib.tlsgpu_owned_workspace_count() == 1
         s.synchronize()
         outs.append((wl.d_wire.download().tobytes(), wl.d_len.download().tobytes(), wl.d_states.download().tobytes()))
         s.close()
-        if k == 2:
-            N.call("tlsgpu_release_workspaces")
+        assert N.lib.tlsgpu_owned_workspace_count() == 0, "stream destroy left its workspace"
     assert all(o == outs[0] for o in outs)
+    # the null stream's buffer lives until tlsgpu_release_workspaces
+    wl.reset_states()
+    seal_dev(d_ch, nch, wl.d_recs, wl.n_records, wl.d_pt, wl.d_wire, wl.d_states, wl.d_len, var, None, None)
+    synchronize()
+    assert wl.d_wire.download().tobytes() == outs[0][0]
+    assert N.lib.tlsgpu_owned_workspace_count() == 1
     N.call("tlsgpu_release_workspaces")
+    assert N.lib.tlsgpu_owned_workspace_count() == 0
+    wl.free()
+
+
+@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES128-SHA", (3, 1)), ("AES128-SHA", (3, 0)),
+                                           ("AES256-SHA", (3, 3)), ("AES256-SHA", (3, 1)), ("AES256-SHA", (3, 0))])
+def test_one_generation_pair_kernel_vs_oracle(suite, version):
+    """Exactly 256 chains per CU: the cfg2 layout (seal_fused_kernel: the pair cipher waves
+    with 8-block groups beside the MAC waves, one generation; tlsgpu_seal_cipher_kernel
+    names it) on mixed records -- empty,
+    sub-block, 15/16/17 blocks (around the 16-block group-alignment threshold), 2G +- 1
+    blocks, 1,434 B, 5,003 B and 16 KiB -- with random content types, badMAC / badPadding
+    faults on ~5 % of the records, and plaintext / wire offsets off the 128-B line so the
+    head blocks before the first whole-line group vary.  Every byte, wire length and final
+    CBC residue / seqnum equals the oracle (tlsrecordlayer.py:538-617, python_aes.py:44)."""
+    _T()
+    from tlslite_amd import _native as N
+    from tlslite_amd import workloads as W
+    from tlslite_amd.device import synchronize
+    from tlslite_amd.recordlayer import seal_cipher_kernel
+    from tests.wl_oracle import device_states, oracle_seal
+    from oracle import oracle as O
+    rng = np.random.default_rng(zlib.crc32(repr(("gen1", suite, version)).encode()))
+    _, kl, ivl, _, ml = O.SUITES[suite]
+    nmin = _many_chains()
+    lens = [0, 1, 15, 16, 17, 15 * 16, 16 * 16, 17 * 16 + 3, 15 * 16 + 9, 31 * 16, 33 * 16 + 1, 1434, 5003, 16384,
+            16 * 8 * 3, 100]
+    groups = []
+    left = nmin
+    for i, n in enumerate(lens):
+        nconn = left if i == len(lens) - 1 else nmin // (2 * len(lens))
+        left -= nconn
+        ivs = np.frombuffer(rng.bytes(ivl * nconn), dtype=np.uint8).reshape(nconn, ivl)
+        recs = 2 if n < 4096 else 1
+        groups.append(W.Group(suite, version, [rng.bytes(kl)], ivs, [rng.bytes(ml)], [rng.bytes(ivl)],
+                              rng.integers(0, 2 ** 40, nconn, dtype=np.uint64), recs, n))
+    nrec = sum(g.nconn * g.recs_per_conn for g in groups)
+    ctype = rng.choice([21, 22, 23], nrec, p=[0.05, 0.05, 0.9])
+    flags = np.where(rng.random(nrec) < 0.05, rng.integers(1, 4, nrec), 0)
+    wl = W.Workload("gen1", groups, 77, rec_ctype=ctype, rec_flags=flags)
+    wl.to_device()
+    assert [n for _, _, n in wl.launches] == [nmin] == [wl.n_chains]
+    var = wl.launches[0][0]
+    assert seal_cipher_kernel(var, nmin).startswith("seal_fused_kernel<%d," % (10 if "128" in suite else 14))
+    wl.launch()
+    synchronize()
+    wire_gpu = wl.d_wire.download()
+    lens_gpu = wl.d_len.download().view(np.int32)
+    states = device_states(wl)
+    wire, lens_o, conns = oracle_seal(wl, nthreads=16)
+    assert lens_gpu.tolist() == lens_o.tolist()
+    bad = np.nonzero(wire_gpu != wire)[0]
+    bad_recs = sorted(set(int(np.searchsorted(wl.wire_off.astype(np.int64), x, side="right")) - 1 for x in bad[:4096]))
+    assert not len(bad), "%d bytes differ, records %s" % (len(bad), bad_recs[:20])
+    bad = [c for c, (s, o) in enumerate(zip(states, conns)) if s.iv != o.iv or s.seqnum != o.seqnum]
+    assert not bad, "chains with a wrong final state: %s" % bad[:10]
     wl.free()

@@ -17,7 +17,7 @@ FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
 OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH = 0, -1, -2, -3, -4, -5
 ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED, ALERT_SKIPPED = -20, -21, -22
 CHAIN_STOP_ON_ALERT = 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 CONN_STATE_BYTES = 2048
 
 
@@ -95,6 +95,7 @@ SIGNATURES = [
     ("tlsgpu_seal_wire_len", _i, [_vp, _u32, ctypes.POINTER(_u32)]),
     ("tlsgpu_seal_workspace_bytes", _sz, [_u32]),
     ("tlsgpu_release_workspaces", _i, []),
+    ("tlsgpu_owned_workspace_count", _sz, []),
     ("tlsgpu_seal_cipher_kernel", _i, [_u32, _u32, ctypes.c_char_p, _sz]),
     ("tlsgpu_seal_dev", _i, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
     ("tlsgpu_pipeline_create", _i, [ctypes.POINTER(_vp), _u32]),

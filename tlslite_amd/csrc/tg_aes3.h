@@ -116,15 +116,13 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 }
 
 // Compile-time experiment switches (tools/build_ab.sh builds them into separate
-// libraries; the product build defines none).  Variants measured slower and not kept
-// (non-temporal loads / stores, v_perm byte-1 addresses, v_cndmask transposes, flat
-// loads, v_and_or 3DES addresses) were removed in round 3; their results are in DESIGN.md
-// and profiles/r02/ab_summary.txt.
-//   TG_AB_NO_MAC     MAC bulk skipped (wrong MACs; timing of the cipher phase alone)
+// libraries; the product build defines none).  Each selects another correct configuration
+// of the product kernels.  Variants measured slower and not kept (non-temporal loads /
+// stores, v_perm byte-1 addresses, v_cndmask transposes, flat loads, v_and_or 3DES
+// addresses) were removed in round 3, and the timing-only probes of the MAC phase (no MAC,
+// MAC without loads / compressions / transposes: wrong output by design) in round 4 (last
+// in commit 4f1633b); their results are in DESIGN.md and profiles/r0{2,3}/.
 //   TG_AB_MAC_PRIO / TG_AB_CBC_PRIO  wave priorities of the MAC / cipher waves
-//   TG_AB_MAC_LOADONLY  cooperative MAC: loads + transposes, no compression (timing only)
-//   TG_AB_MAC_NOLOAD    cooperative MAC: compressions on register data, no loads (timing only)
-//   TG_AB_MAC_NOTRANS   cooperative MAC: no quad transposes (timing only: what they cost)
 //   TG_AB_MAC_PF        chunks the cooperative MAC loop prefetches (default 2)
 //   TG_AB_MAC_LB        mac_kernel's launch bound in 256-thread blocks per CU (default 3)
 //   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
@@ -133,6 +131,9 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_MAC_LB_MANY / TG_AB_MAC_PF_MANY  launch bound / prefetch ring of the many-chains MAC kernel
 //   TG_AB_NO_PAIR    cipher phase on the quad layout (cbc_kernel) in the throughput regimes too,
 //                    instead of 2 lanes per chain (cbc_pair_kernel)
+//   TG_AB_SPLIT_PAIR the split prefix / MAC / cbc_pair_kernel path in the pair regime instead of
+//                    seal_fused_kernel (tg_fused.h); TG_AB_FUSED_G / TG_AB_FUSED_GM: the fused
+//                    kernel's prefetch group in the one-generation / many-chains regime
 //   TG_AB_PAIR_G1 / TG_AB_PAIR_GM  the pair kernel's prefetch group (blocks) in the one-generation
 //                    (cfg2) / many-chains (cfg3) regime; TG_AB_PAIR_MAC_MANY: the 128-VGPR MAC
 //                    kernel in the one-generation pair regime too
@@ -249,11 +250,7 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
     for (int d = 0; d < PF; d++)
 #pragma unroll
         for (int L = 0; L < 4; L++) {
-#ifdef TG_AB_MAC_NOLOAD
-            nxt[d][L] = make_uint4(lo + L + d, hi, q, L);
-#else
             nxt[d][L] = ldg16(PL[L] + 64 * min((uint32_t)d, NL[L]));
-#endif
         }
     // The loop is unrolled by PF with ring slot k fixed per unrolled step: slot k's chunk is
     // transposed out first and its registers reloaded straight away, so no register copies
@@ -277,17 +274,6 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
             x[0] = nxt[k][0].w; x[1] = nxt[k][1].w; x[2] = nxt[k][2].w; x[3] = nxt[k][3].w;
             quad_transpose4(x, q);
             d[3] = x[0]; d[7] = x[1]; d[11] = x[2]; d[15] = x[3];
-#ifdef TG_AB_MAC_NOTRANS  // timing only: the loaded words as they are (wrong MACs)
-#pragma unroll
-            for (int L = 0; L < 4; L++) {
-                d[4 * L] = nxt[k][L].x; d[4 * L + 1] = nxt[k][L].y; d[4 * L + 2] = nxt[k][L].z; d[4 * L + 3] = nxt[k][L].w;
-            }
-#endif
-#ifdef TG_AB_MAC_NOLOAD
-#pragma unroll
-            for (int L = 0; L < 4; L++)
-                nxt[k][L] = make_uint4(nxt[k][L].y + c, nxt[k][L].z ^ c, nxt[k][L].w, nxt[k][L].x);
-#else
             // the ring is reloaded as a whole after its last slot is transposed: a record's
             // consecutive 64-B chunks (whole 128-B lines) are requested back to back rather than
             // one compression apart (cfg2 901-902 -> 916-918 GiB/s with PF = 2)
@@ -297,17 +283,7 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
 #pragma unroll
                     for (int L = 0; L < 4; L++) nxt[kk][L] = ldg16(PL[L] + 64 * min(c0 + kk + PF, NL[L]));
             }
-#endif
-#ifdef TG_AB_MAC_LOADONLY
-            if (c < nfull) {
-                uint32_t a = 0;
-#pragma unroll
-                for (int i = 0; i < 16; i++) a ^= d[i];
-                mac.h[0] ^= a;
-            }
-#else
             if (c < nfull) mac.update(d);
-#endif
         }
     }
 }
@@ -353,14 +329,12 @@ __global__ void __launch_bounds__(256, LB) mac_kernel(const tlsgpu_record* __res
     uint32_t coop = (act && al16 && nfull) ? 1u : 0u;
     coop &= quad_dpp<0xB1>(coop);
     coop &= quad_dpp<0x4E>(coop);
-#ifndef TG_AB_NO_MAC
     if (coop) {
         mac_bulk_coop<PF>(mac, P, nfull, threadIdx.x & 3u);
     } else if (act) {
         if (al16) mac_bulk<true>(mac, P, nfull);
         else mac_bulk<false>(mac, P, nfull);
     }
-#endif
     if (!act) return;
     const uint32_t E = st->explicit_iv ? (uint32_t)BS : 0u;
     const uint32_t cur0 = E + n + DL;
@@ -620,10 +594,17 @@ constexpr int PAIR_WAVES_MANY = TG_AB_PAIR_WM;
 #define TG_AB_PAIR_GM 4
 #endif
 
-template <int NR, int G, bool AL, bool CLAMP>
+// Progress hook of the cipher's plaintext loads: the fused seal kernel (tg_fused.h) tells its
+// MAC waves how far a chain's loads have been issued (NoPub: the split path, nothing to tell).
+struct NoPub {
+    __device__ __forceinline__ void operator()(uint32_t /*blocks issued in the bulk*/) const {}
+};
+
+template <int NR, int G, bool AL, bool CLAMP, class Pub = NoPub>
 __device__ __forceinline__ void pcbc_group(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
                                            const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
-                                           uint8_t* O, uint32_t b0, uint32_t last, uint2 f[G]) {
+                                           uint8_t* O, uint32_t b0, uint32_t last, uint2 f[G],
+                                           const Pub& pub = Pub()) {
     constexpr int PAIR_G = G;
     uint2 c[PAIR_G];
 #pragma unroll
@@ -639,6 +620,7 @@ __device__ __forceinline__ void pcbc_group(const PairAes& aes, const uint32_t* k
 #pragma unroll
         for (int i = 0; i < PAIR_G; i++) f[i] = ld64t<AL>(Pn + 16 * i);
     }
+    pub(CLAMP ? last + 1 : b0 + 2 * PAIR_G);  // blocks of P (this bulk) whose loads are issued
     uint8_t* Ob = O + 16 * b0;
     // the group's ciphertext is kept in registers and stored at the group's end: the chain's
     // stores reach the L2 together and merge into whole lines (with aligned groups, pcbc_bulk)
@@ -654,10 +636,19 @@ __device__ __forceinline__ void pcbc_group(const PairAes& aes, const uint32_t* k
 
 constexpr uint32_t PAIR_ALIGN_MIN = 16;  // blocks: records this long align their groups
 
-template <int NR, int GI, bool AL>
+// Pub: called with the number of the record's blocks whose loads are issued (the hook is
+// handed the group loop's counts shifted by the head)
+template <class Pub>
+struct PubShift {
+    const Pub& pub;
+    uint32_t head;
+    __device__ __forceinline__ void operator()(uint32_t b) const { pub(head + b); }
+};
+
+template <int NR, int GI, bool AL, class Pub = NoPub>
 __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
                                           const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
-                                          uint8_t* O, uint32_t nb) {
+                                          uint8_t* O, uint32_t nb, const Pub& pub = Pub()) {
     if (nb == 0) return;
     constexpr uint32_t G = GI;
     // Records of at least PAIR_ALIGN_MIN blocks first run the head blocks up to the output's
@@ -686,6 +677,8 @@ __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw
 #pragma unroll
         for (int i = 0; i < (int)G; i++) f[i] = ld64t<AL>(Pg + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
     }
+    pub(head + (ng < G ? ng : G));
+    const PubShift<Pub> gpub{pub, head};
 #pragma unroll
     for (int i = 0; i < (int)G; i++)
         if ((uint32_t)i < head) {
@@ -695,11 +688,12 @@ __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw
     if (ng == 0) return;
     uint32_t b0 = 0;
     if (ng >= 2 * G) {  // first group peeled, as cbc_bulk
-        pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, 0, last, f);
-        for (b0 = G; b0 + 2 * G <= ng; b0 += G) pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f);
+        pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, 0, last, f, gpub);
+        for (b0 = G; b0 + 2 * G <= ng; b0 += G)
+            pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f, gpub);
     }
     if (b0 + G <= ng) {
-        pcbc_group<NR, GI, AL, true>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f);
+        pcbc_group<NR, GI, AL, true>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f, gpub);
         b0 += G;
     }
 #pragma unroll

@@ -60,6 +60,8 @@ inline ConnState* S(tlsgpu_conn_state* p) { return reinterpret_cast<ConnState*>(
 inline const ConnState* S(const tlsgpu_conn_state* p) { return reinterpret_cast<const ConnState*>(p); }
 inline hipStream_t HS(tlsgpu_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
+hipError_t own_release_stream(hipStream_t s);
+
 }  // namespace
 
 extern "C" {
@@ -142,6 +144,11 @@ int tlsgpu_stream_create(tlsgpu_stream* s) {
     return 0;
 }
 int tlsgpu_stream_destroy(tlsgpu_stream s) {
+    if (!s) return fail(TLSGPU_EINVAL, "the null stream cannot be destroyed");
+    TG_HIP(hipStreamSynchronize(HS(s)));
+    // the library-owned workspaces of this stream go with it
+    hipError_t e = own_release_stream(HS(s));
+    if (e != hipSuccess) return fail_hip(e, "tlsgpu_stream_destroy: workspace release");
     TG_HIP(hipStreamDestroy(HS(s)));
     return 0;
 }
@@ -258,9 +265,11 @@ int tlsgpu_seal_cipher_kernel(uint32_t variant, uint32_t nchains, char* name, si
 
 
 // library-owned workspace: one grow-only buffer per (kind, device, stream), so calls
-// on different streams never share one and calls on one stream are ordered by it;
-// tlsgpu_release_workspaces() frees them all (a caller that creates and destroys many
-// streams calls it, or the buffers live until the process ends)
+// on different streams never share one and calls on one stream are ordered by it.  The
+// device is the stream's (hipStreamGetDevice).  tlsgpu_stream_destroy frees the buffers of
+// the stream it destroys (a later stream that reuses the handle value starts without
+// one); tlsgpu_release_workspaces() frees them all.
+}  // extern "C"
 namespace {
 struct OwnKey {
     int kind, dev;
@@ -275,40 +284,67 @@ struct OwnBuf {
 };
 std::mutex own_mu;
 std::map<OwnKey, OwnBuf> own_bufs;
+
+// frees the buffers `pick` selects and erases their entries whatever fails on the way (an
+// entry is never left pointing at freed memory); returns the first error
+template <class Pick>
+hipError_t own_release(Pick pick, bool sync_device) {
+    hipError_t first = hipSuccess;
+    std::set<int> synced;
+    for (auto it = own_bufs.begin(); it != own_bufs.end();) {
+        if (!pick(it->first)) {
+            ++it;
+            continue;
+        }
+        const int dev = it->first.dev;
+        DeviceGuard guard(dev);
+        // the buffer's stream may already be gone: wait for its whole device once
+        if (sync_device && !synced.count(dev)) {
+            hipError_t e = hipDeviceSynchronize();
+            if (e != hipSuccess && first == hipSuccess) first = e;
+            synced.insert(dev);
+        }
+        hipError_t e = it->second.p ? hipFree(it->second.p) : hipSuccess;
+        if (e != hipSuccess && first == hipSuccess) first = e;
+        it = own_bufs.erase(it);
+    }
+    return first;
+}
 }  // namespace
+
+namespace {
+hipError_t own_release_stream(hipStream_t s) {
+    std::lock_guard<std::mutex> g(own_mu);
+    return own_release([s](const OwnKey& k) { return k.s == s; }, false);  // s is synchronised
+}
+}  // namespace
+extern "C" {
 
 int tlsgpu_release_workspaces(void) {
     std::lock_guard<std::mutex> g(own_mu);
-    int cur = 0;
-    TG_HIP(hipGetDevice(&cur));
-    std::set<int> synced;
-    for (auto& kv : own_bufs) {
-        // the stream may be gone: wait for the whole device once before freeing its buffers
-        if (!synced.count(kv.first.dev)) {
-            TG_HIP(hipSetDevice(kv.first.dev));
-            TG_HIP(hipDeviceSynchronize());
-            synced.insert(kv.first.dev);
-        }
-        TG_HIP(hipSetDevice(kv.first.dev));
-        TG_HIP(hipFree(kv.second.p));
-    }
-    own_bufs.clear();
-    TG_HIP(hipSetDevice(cur));
+    hipError_t e = own_release([](const OwnKey&) { return true; }, true);
+    if (e != hipSuccess) return fail_hip(e, "tlsgpu_release_workspaces");
     return 0;
 }
 
+size_t tlsgpu_owned_workspace_count(void) {
+    std::lock_guard<std::mutex> g(own_mu);
+    return own_bufs.size();
+}
+
 static int own_workspace(int kind, size_t need, hipStream_t stream, uint8_t** out) {
-    int dev = 0;
-    TG_HIP(hipGetDevice(&dev));
+    const int dev = stream_device(stream);
     std::lock_guard<std::mutex> g(own_mu);
     OwnBuf& b = own_bufs[OwnKey{kind, dev, stream}];
     if (b.bytes < need) {
+        DeviceGuard guard(dev);
         if (b.p) {
             TG_HIP(hipStreamSynchronize(stream));  // earlier calls on this stream may still read it
-            TG_HIP(hipFree(b.p));
+            void* old = b.p;
+            b.p = nullptr;
+            b.bytes = 0;
+            TG_HIP(hipFree(old));
         }
-        b.p = nullptr;
-        b.bytes = 0;
         TG_HIP(hipMalloc(&b.p, need));
         b.bytes = need;
     }

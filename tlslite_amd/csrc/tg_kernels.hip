@@ -9,12 +9,14 @@
 //   fill_kernel      deterministic synthetic input (splitmix64 byte stream)
 // The library has exactly one kernel per (direction, suite variant): no runtime
 // selection between implementations.
+#include <atomic>
 #include <mutex>
 #include <set>
 #include <utility>
 #include "tg_device.h"
 #include "tg_quad.h"
 #include "tg_aes3.h"
+#include "tg_fused.h"
 #include "tg_open3.h"
 #include "tg_derive.h"
 #include "tg_launch.h"
@@ -270,43 +272,56 @@ __global__ void __launch_bounds__(SEAL_BLOCK) rc4_open_kernel(const tlsgpu_chain
 }
 
 // ---------------------------------------------------------------- launch plumbing
-// hipFuncSetAttribute is per device: remember which (kernel, device) pairs have it
-static hipError_t set_lds(const void* kern, uint32_t bytes) {
+// The device a launch runs on is its stream's (hipStreamGetDevice), not the calling
+// thread's current device: a caller may hold streams of several GPUs.  The null stream
+// belongs to the current device.
+int stream_device(hipStream_t s) {
+    int dev = 0;
+    if (s) {
+        hipDevice_t d = 0;
+        if (hipStreamGetDevice(s, &d) == hipSuccess) return (int)d;
+        (void)hipGetLastError();
+    }
+    (void)hipGetDevice(&dev);
+    return dev;
+}
+
+// hipFuncSetAttribute is per device: remember which (kernel, device) pairs have it; the
+// attribute is set with the stream's device current
+static hipError_t set_lds(const void* kern, uint32_t bytes, hipStream_t s) {
     static std::mutex mu;
     static std::set<std::pair<const void*, int>> done;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return e;
+    const int dev = stream_device(s);
     std::lock_guard<std::mutex> g(mu);
     if (done.count({kern, dev})) return hipSuccess;
-    e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    DeviceGuard guard(dev);
+    hipError_t e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
     if (e == hipSuccess) done.insert({kern, dev});
     return e;
 }
 template <class K>
-static hipError_t set_lds(K kern, uint32_t bytes) {
-    return set_lds(reinterpret_cast<const void*>(kern), bytes);
+static hipError_t set_lds(K kern, uint32_t bytes, hipStream_t s) {
+    return set_lds(reinterpret_cast<const void*>(kern), bytes, s);
 }
 
-// CUs of the current device (cached per device)
-static uint32_t cu_count() {
-    static int ncu[64] = {0};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    dev &= 63;
-    if (!ncu[dev]) {
-        int n = 0;
+// CUs of the stream's device (cached per device)
+static uint32_t cu_count(hipStream_t s) {
+    static std::atomic<int> ncu[64];
+    const int dev = stream_device(s) & 63;
+    int n = ncu[dev].load(std::memory_order_relaxed);
+    if (!n) {
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        ncu[dev] = n > 0 ? n : 256;
+        n = n > 0 ? n : 256;
+        ncu[dev].store(n, std::memory_order_relaxed);
     }
-    return (uint32_t)ncu[dev];
+    return (uint32_t)n;
 }
 
 template <int MAC, bool SSL3>
 static hipError_t launch_rc4_open(const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
                                   const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s) {
     auto kern = rc4_open_kernel<MAC, SSL3>;
-    hipError_t e = set_lds(kern, RC4_LDS_BYTES);
+    hipError_t e = set_lds(kern, RC4_LDS_BYTES, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((n + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), RC4_LDS_BYTES, s, chains, n, recs,
                        wire, pt, states, status);
@@ -343,22 +358,22 @@ size_t seal_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * (size
 
 // AES batches with more chains than one generation of 16-wave cipher workgroups: the
 // many-chains configuration (C3_WAVES_MANY cipher waves, MAC kernel at MAC_LB_MANY)
-static bool many_chains(uint32_t nchains) {
+static bool many_chains(uint32_t nchains, hipStream_t s) {
 #ifdef TG_AB_NO_MANY
     return false;
 #else
-    return nchains > (uint32_t)C3_CHAINS * cu_count();
+    return nchains > (uint32_t)C3_CHAINS * cu_count(s);
 #endif
 }
 
 // The AES cipher phase runs 2 lanes per chain (cbc_pair_kernel) when every CU gets at
 // least a full workgroup of chains (C3_CHAINS = 256: cfg2, cfg3), the quad layout
 // (cbc_kernel, latency form) with fewer (cfg4's 2-16 chains per CU).
-static bool pair_regime(uint32_t nchains) {
+static bool pair_regime(uint32_t nchains, hipStream_t s) {
 #ifdef TG_AB_NO_PAIR
     return false;
 #else
-    return nchains >= (uint32_t)C3_CHAINS * cu_count();
+    return nchains >= (uint32_t)C3_CHAINS * cu_count(s);
 #endif
 }
 
@@ -383,9 +398,9 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
                        recs, states, wire_len, meta, nrecords, epoch, sb.wire_cap);
     const dim3 grid((r1 - r0 + 255) / 256);
 #ifdef TG_AB_PAIR_MAC_MANY
-    const bool mac_many = NR != 0 && nchains >= (uint32_t)C3_CHAINS * cu_count();
+    const bool mac_many = NR != 0 && nchains >= (uint32_t)C3_CHAINS * cu_count(s);
 #else
-    const bool mac_many = NR != 0 && many_chains(nchains);
+    const bool mac_many = NR != 0 && many_chains(nchains, s);
 #endif
     // (many chains: two 128-VGPR MAC waves per SIMD fit beside the cipher waves; beside the
     // two 88-VGPR pair waves the 168-VGPR kernel would fit two too -- measured the same on
@@ -399,25 +414,60 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
     return hipGetLastError();
 }
 
+// The AES seal in one kernel (tg_fused.h) in the pair regime: every CU gets a full
+// 256-chain workgroup (cfg2, cfg3), so the cipher's and the MAC's reads of the plaintext can
+// be one.  TG_AB_SPLIT_PAIR: the split prefix / MAC / cipher kernels there too (A/B builds).
+static bool fused_regime(uint32_t nchains, hipStream_t s) {
+#ifdef TG_AB_SPLIT_PAIR
+    return false;
+#else
+    return pair_regime(nchains, s);
+#endif
+}
+#ifndef TG_AB_FUSED_G
+#define TG_AB_FUSED_G 8
+#endif
+#ifndef TG_AB_FUSED_GM
+#define TG_AB_FUSED_GM 8
+#endif
+
+template <int NR, int MAC, bool SSL3>
+static hipError_t launch_fused(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
+                               uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
+                               int32_t* wire_len, uint64_t wire_cap, hipStream_t s) {
+    const uint32_t ncu = cu_count(s);
+    uint32_t cpw = (nchains + ncu - 1) / ncu;
+    cpw = cpw > (uint32_t)FZ_SLOTS ? (uint32_t)FZ_SLOTS : cpw;
+    uint32_t grid = (nchains + cpw - 1) / cpw;
+    grid = grid > ncu ? ncu : grid;
+    const bool many = many_chains(nchains, s);
+    auto kern = many ? seal_fused_kernel<NR, MAC, SSL3, TG_AB_FUSED_GM> : seal_fused_kernel<NR, MAC, SSL3, TG_AB_FUSED_G>;
+    hipError_t e = set_lds(kern, FZ_LDS_BYTES, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(FZ_THREADS), FZ_LDS_BYTES, s, chains, nchains, recs, nrecords, pt, wire,
+                       states, wire_len, cpw, wire_cap);
+    return hipGetLastError();
+}
+
 // phase 2 (stream s2, after phase 1): CBC over [explicit IV | P blocks | tail]
 template <int NR>
 static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
                                    uint8_t* ws, uint32_t epoch, hipStream_t s) {
-    const uint32_t ncu = cu_count();
+    const uint32_t ncu = cu_count(s);
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
     if constexpr (NR == 0) {  // 3DES: 4 lanes per chain
         uint32_t pw = (nchains + ncu - 1) / ncu;
         pw = pw < 1 ? 1 : (pw > (uint32_t)D4_CHAINS ? (uint32_t)D4_CHAINS : pw);
-        hipError_t e = set_lds(tdes4_kernel, D4_LDS_BYTES);
+        hipError_t e = set_lds(tdes4_kernel, D4_LDS_BYTES, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(tdes4_kernel, dim3((nchains + pw - 1) / pw), dim3(D4_THREADS), D4_LDS_BYTES, s, chains,
                            nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch);
         return hipGetLastError();
     } else {
-        const bool many = many_chains(nchains);
-        if (pair_regime(nchains)) {
+        const bool many = many_chains(nchains, s);
+        if (pair_regime(nchains, s)) {
             // a CU gets at least a workgroup's worth of chains: 2 lanes per chain
             const uint32_t waves = many ? PAIR_WAVES_MANY : PAIR_WAVES;
             const uint32_t pwg = 32u * waves;
@@ -425,7 +475,7 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
             cpw = cpw > pwg ? pwg : cpw;
             auto kern = many ? cbc_pair_kernel<NR, PAIR_WAVES_MANY, TG_AB_PAIR_GM>
                              : cbc_pair_kernel<NR, PAIR_WAVES, TG_AB_PAIR_G1>;
-            hipError_t e = set_lds(kern, AES_LDS_BYTES);
+            hipError_t e = set_lds(kern, AES_LDS_BYTES, s);
             if (e != hipSuccess) return e;
             uint32_t grid = (nchains + cpw - 1) / cpw;
             grid = grid > ncu ? ncu : grid;
@@ -439,7 +489,7 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         // fewer chains than a workgroup's quads: the latency form of the AES round
         auto kern = many ? cbc_kernel<NR, false, C3_WAVES_MANY>
                          : cpw < (uint32_t)C3_CHAINS ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
-        hipError_t e = set_lds(kern, AES_LDS_BYTES);
+        hipError_t e = set_lds(kern, AES_LDS_BYTES, s);
         if (e != hipSuccess) return e;
         // persistent: at most one workgroup per CU, quads loop over chain generations
         uint32_t grid = (nchains + cpw - 1) / cpw;
@@ -458,10 +508,16 @@ std::string seal_cipher_kernel(uint32_t variant, uint32_t nchains) {
     if (c == TLSGPU_CIPHER_3DES) return "tdes4_kernel";
     if (c != TLSGPU_CIPHER_AES128 && c != TLSGPU_CIPHER_AES256) return "";
     const int nr = c == TLSGPU_CIPHER_AES128 ? 10 : 14;
-    const uint32_t ncu = cu_count();
-    const bool many = many_chains(nchains);
+    const uint32_t ncu = cu_count(nullptr);
+    const bool many = many_chains(nchains, nullptr);
     char b[64];
-    if (pair_regime(nchains)) {
+    if (fused_regime(nchains, nullptr)) {
+        const uint32_t m = (variant >> 8) & 0xff, ssl3 = (variant >> 16) & 1;
+        snprintf(b, sizeof b, "seal_fused_kernel<%d, %u, %s, %d>", nr, m, ssl3 ? "true" : "false",
+                 many ? TG_AB_FUSED_GM : TG_AB_FUSED_G);
+        return b;
+    }
+    if (pair_regime(nchains, nullptr)) {
         snprintf(b, sizeof b, "cbc_pair_kernel<%d, %d, %d>", nr, many ? PAIR_WAVES_MANY : PAIR_WAVES,
                  many ? TG_AB_PAIR_GM : TG_AB_PAIR_G1);
         return b;
@@ -492,6 +548,18 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
     *known = true;
     hipError_t e = hipSuccess;
 #define TG_PH(CID, NR, MAC_ID, SSL3)                                                                            \
+    if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3) && NR != 0 && fused_regime(nchains, s2)) {                  \
+        /* one kernel on the cipher stream, ordered after whatever s1 waits for (host pipeline: H2D) */          \
+        if (s2 != s1) {                                                                                          \
+            if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                      \
+            if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                               \
+        }                                                                                                        \
+        if (cbc_start && (e = hipEventRecord(cbc_start, s2)) != hipSuccess) return e;                           \
+        e = launch_fused<NR == 0 ? 10 : NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states,      \
+                                                         wire_len, sb.wire_cap, s2);                             \
+        if (e == hipSuccess && cbc_stop) e = hipEventRecord(cbc_stop, s2);                                       \
+        return e;                                                                                                \
+    }                                                                                                            \
     if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3)) {                                                          \
         e = launch_mac_phase<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,   \
                                                epoch, s1, sb);                                                   \
@@ -516,7 +584,7 @@ static hipError_t launch_rc4_seal(const tlsgpu_chain* chains, uint32_t nchains, 
                                   const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
                                   hipStream_t s) {
     auto kern = rc4_seal_kernel<MAC, SSL3>;
-    hipError_t e = set_lds(kern, RC4_LDS_BYTES);
+    hipError_t e = set_lds(kern, RC4_LDS_BYTES, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((nchains + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), RC4_LDS_BYTES, s, chains,
                        nchains, recs, pt, wire, states, wire_len);
@@ -555,7 +623,7 @@ static hipError_t launch_cipher_t(const tlsgpu_span* spans, uint32_t n, const ui
                          CIPHER == TLSGPU_CIPHER_AES192;
     constexpr uint32_t lds = AES ? (DEC ? AES_DEC_LDS_BYTES : AES_LDS_BYTES)
                                  : CIPHER == TLSGPU_CIPHER_3DES ? DES_LDS_BYTES : RC4_LDS_BYTES;
-    hipError_t e = set_lds(kern, lds);
+    hipError_t e = set_lds(kern, lds, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((n + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), lds, s, spans, n, in, out,
                        states);
@@ -618,16 +686,16 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
     hipLaunchKernelGGL((open_prefix_kernel<CID, MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords,
                        wire, states, status, meta, epoch);
     if constexpr (NR == 0) {
-        if ((e = set_lds(open_tdes_kernel, DES_LDS_BYTES)) != hipSuccess) return e;
+        if ((e = set_lds(open_tdes_kernel, DES_LDS_BYTES, s)) != hipSuccess) return e;
         uint32_t grid = (nrecords + (OT_THREADS / 64) - 1) / (OT_THREADS / 64);
-        grid = grid > cu_count() ? cu_count() : (grid ? grid : 1u);
+        grid = grid > cu_count(s) ? cu_count(s) : (grid ? grid : 1u);
         hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire, pt,
                            states, meta, epoch);
     } else {
         auto dec = open_aes_kernel<NR == 0 ? 10 : NR>;
-        if ((e = set_lds(dec, AES_DEC_LDS_BYTES)) != hipSuccess) return e;
+        if ((e = set_lds(dec, AES_DEC_LDS_BYTES, s)) != hipSuccess) return e;
         uint32_t grid = (nrecords + (O3_THREADS / 64) - 1) / (O3_THREADS / 64);
-        grid = grid > cu_count() ? cu_count() : (grid ? grid : 1u);
+        grid = grid > cu_count(s) ? cu_count(s) : (grid ? grid : 1u);
         hipLaunchKernelGGL(dec, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s, recs, nrecords, wire, pt, states,
                            meta, epoch);
     }

@@ -8,6 +8,23 @@ namespace tg {
 
 constexpr int SEAL_BLOCK = 256;  // one lane per chain, 4 waves per workgroup
 
+// The device of a stream (the current device for the null stream): launch plumbing keys
+// its per-device caches and allocations on it, not on the calling thread's current device.
+int stream_device(hipStream_t s);
+// Makes `dev` the current device for a scope and restores the previous one.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        int cur = 0;
+        if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 size_t seal_workspace_bytes(uint32_t nrecords);
 // What a split-path seal launch may touch besides its chains: the window of records its
 // chains use ([rec_lo, rec_hi): the MAC phase's grid and meta clear cover only it) and the

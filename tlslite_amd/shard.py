@@ -8,7 +8,13 @@ sum-over-ranks of its timing numbers and a gather of check digests.  That is
 done by a small TCP rendezvous of our own (no PyTorch, no RCCL): rank 0 serves
 `MASTER_ADDR:(MASTER_PORT + 1)` -- `torch.distributed.run` keeps its own store on
 MASTER_PORT itself -- (or `TLSGPU_RDZV_PORT`), every other rank connects, and
-each collective is an all-gather of byte strings through rank 0."""
+each collective is an all-gather of byte strings through rank 0.
+
+A rank's hello carries a shared token (TLSGPU_RDZV_TOKEN, which bench.py's own rank
+spawner sets, else torch.distributed.run's TORCHELASTIC_RUN_ID): rank 0 drops
+connections that do not present it.  Sockets keep a finite timeout after set-up, so a
+rank that hangs ends the others with an error instead of blocking them forever."""
+import errno
 import os
 import socket
 import struct
@@ -52,7 +58,7 @@ class ShardGroup:
     """RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT from the
     environment (as torch.distributed.run sets them); world size 1 needs none."""
 
-    def __init__(self, timeout=120.0):
+    def __init__(self, timeout=120.0, op_timeout=900.0):
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.local = int(os.environ.get("LOCAL_RANK", str(self.rank)))
@@ -62,21 +68,40 @@ class ShardGroup:
             return
         addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = int(os.environ.get("TLSGPU_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
+        token = (os.environ.get("TLSGPU_RDZV_TOKEN") or os.environ.get("TORCHELASTIC_RUN_ID") or "").encode()[:255]
         deadline = time.monotonic() + timeout
         if self.rank == 0:
             srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-            srv.bind((addr, port))
-            srv.listen(self.world)
-            srv.settimeout(timeout)
+            try:
+                srv.bind((addr, port))
+            except OSError as e:
+                if e.errno == errno.EADDRINUSE:
+                    raise RuntimeError("rendezvous: %s:%d is in use (MASTER_PORT + 1 by default); set TLSGPU_RDZV_PORT "
+                                       "to a free port" % (addr, port)) from e
+                raise
+            srv.listen(self.world + 4)
             by_rank = {}
             while len(by_rank) < self.world - 1:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    raise TimeoutError("rendezvous: %d of %d ranks joined" % (len(by_rank) + 1, self.world))
+                srv.settimeout(left)
                 c, _ = srv.accept()
-                c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                c.settimeout(None)
-                (r,) = struct.unpack("<I", _recv_exact(c, 4))
+                c.settimeout(10.0)
+                try:
+                    (r, n) = struct.unpack("<IB", _recv_exact(c, 5))
+                    tok = _recv_exact(c, n) if n else b""
+                except (OSError, ConnectionError, struct.error):
+                    c.close()
+                    continue
+                if tok != token:  # not one of this job's ranks
+                    c.close()
+                    continue
                 if r in by_rank or not 0 < r < self.world:
                     raise RuntimeError("rendezvous: unexpected rank %d" % r)
+                c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                c.settimeout(op_timeout)
                 by_rank[r] = c
             srv.close()
             self._peers = [by_rank[r] for r in range(1, self.world)]
@@ -90,8 +115,8 @@ class ShardGroup:
                         raise
                     time.sleep(0.05)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            s.settimeout(None)
-            s.sendall(struct.pack("<I", self.rank))
+            s.settimeout(op_timeout)
+            s.sendall(struct.pack("<IB", self.rank, len(token)) + token)
             self._sock = s
 
     def all_gather(self, b):

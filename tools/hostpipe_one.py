@@ -11,9 +11,6 @@ from tlslite_amd.device import PinnedBuffer, synchronize  # noqa: E402
 from tlslite_amd.recordlayer import HostSealPipeline, make_chains, make_records  # noqa: E402
 
 chunk, depth = int(sys.argv[1]) << 20, int(sys.argv[2])
-if len(sys.argv) > 3 and sys.argv[3] == "torchpool":  # an application that already uses torch streams
-    import torch
-    _pool = [torch.cuda.Stream(priority=p) for p in (0, -1) for _ in range(4)]
 wl = W.cfg2()
 wl.to_device()
 var = wl.launches[0][0]

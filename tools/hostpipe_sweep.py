@@ -5,7 +5,6 @@ import sys
 import time
 
 import numpy as np
-import torch
 
 sys.path.insert(0, ".")
 from tlslite_amd import workloads as W  # noqa: E402
@@ -17,26 +16,10 @@ GIB = 1 << 30
 
 
 def raw_copies(nbytes):
-    h1 = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    h2 = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    d1 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    d2 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    res = {}
-    for name, both in (("h2d", 1), ("d2h", 2), ("both", 3)):
-        best = 1e9
-        for _ in range(3):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            if both & 1:
-                with torch.cuda.stream(s1):
-                    d1.copy_(h1, non_blocking=True)
-            if both & 2:
-                with torch.cuda.stream(s2):
-                    h2.copy_(d2, non_blocking=True)
-            torch.cuda.synchronize()
-            best = min(best, time.perf_counter() - t0)
-        res[name] = nbytes * (2 if both == 3 else 1) / best / 1e9
+    """Raw pinned copy rates through the HIP runtime (bench.py's pcie_rates)."""
+    sys.path.insert(0, ".")
+    from bench import pcie_rates
+    res = pcie_rates(nbytes)
     print("raw pinned copies of %d MiB: H2D %.1f GB/s, D2H %.1f GB/s, both at once %.1f GB/s total"
           % (nbytes >> 20, res["h2d"], res["d2h"], res["both"]), flush=True)
 

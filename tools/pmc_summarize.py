@@ -24,7 +24,7 @@ NCU = 256
 # bench set-up: synthetic plaintext fill, buffer zeroing, state resets and the copy-rate
 # measurement (d2d copies) -- not the seal call
 SETUP = ("fill_kernel", "__amd_rocclr_fillBuffer", "__amd_rocclr_copyBuffer")
-DOMINANT = ("cbc_pair_kernel", "cbc_kernel", "rc4_seal_kernel", "tdes4_kernel")
+DOMINANT = ("seal_fused_kernel", "cbc_pair_kernel", "cbc_kernel", "rc4_seal_kernel", "tdes4_kernel")
 
 
 def stem(name):
@@ -60,6 +60,19 @@ for f in glob.glob(os.path.join(out, "g*", "**", "*kernel_trace.csv"), recursive
         durations.setdefault(stem(r["Kernel_Name"]), []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 
 res = {"config": cfg, "kernels": {}}
+# the workload the passes sealed (bench.py's JSON line in each pass's log): bench.py attaches
+# this file's traffic only to runs of the same workload and record count
+for f in sorted(glob.glob(os.path.join(out, "g*.log"))):
+    for line in open(f, errors="replace"):
+        if line.startswith("{"):
+            try:
+                d = json.loads(line)
+            except ValueError:
+                continue
+            res["workload"] = d["config"]["workload"]
+            res["records"] = d["config"]["records_per_gpu"]
+    if "workload" in res:
+        break
 for k, cs in counters.items():
     row = {}
     for c, vals in cs.items():
