@@ -492,9 +492,8 @@ def test_library_workspaces_released_and_reallocated():
 @pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES128-SHA", (3, 1)), ("AES128-SHA", (3, 0)),
                                            ("AES256-SHA", (3, 3)), ("AES256-SHA", (3, 1)), ("AES256-SHA", (3, 0))])
 def test_one_generation_pair_kernel_vs_oracle(suite, version):
-    """Exactly 256 chains per CU: the cfg2 layout (seal_fused_kernel: the pair cipher waves
-    with 8-block groups beside the MAC waves, one generation; tlsgpu_seal_cipher_kernel
-    names it) on mixed records -- empty,
+    """Exactly 256 chains per CU: the cfg2 cipher layout (cbc_pair_kernel with 8-block
+    groups, one generation; tlsgpu_seal_cipher_kernel names it) on mixed records -- empty,
     sub-block, 15/16/17 blocks (around the 16-block group-alignment threshold), 2G +- 1
     blocks, 1,434 B, 5,003 B and 16 KiB -- with random content types, badMAC / badPadding
     faults on ~5 % of the records, and plaintext / wire offsets off the 128-B line so the
@@ -528,7 +527,7 @@ def test_one_generation_pair_kernel_vs_oracle(suite, version):
     wl.to_device()
     assert [n for _, _, n in wl.launches] == [nmin] == [wl.n_chains]
     var = wl.launches[0][0]
-    assert seal_cipher_kernel(var, nmin).startswith("seal_fused_kernel<%d," % (10 if "128" in suite else 14))
+    assert seal_cipher_kernel(var, nmin).startswith("cbc_pair_kernel<%d, 8, 8>" % (10 if "128" in suite else 14))
     wl.launch()
     synchronize()
     wire_gpu = wl.d_wire.download()

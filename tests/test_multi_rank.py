@@ -218,3 +218,54 @@ def test_shard_rendezvous_three_ranks():
         assert res[r]["sum"] == 0.5 + 1.5 + 2.5
         assert res[r]["gather"] == [b"\x00", b"\x01\x01", b"\x02\x02\x02"]
         assert res[r]["dev"] == r % 2
+
+
+def _token_rank0(port, q):
+    os.environ.update(RANK="0", WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port - 1),
+                      TLSGPU_RDZV_TOKEN="job-a")
+    from tlslite_amd.shard import ShardGroup
+    g = ShardGroup(timeout=60)
+    q.put(g.sum(1.0))
+    g.close()
+
+
+def _token_rank1(port, q):
+    os.environ.update(RANK="1", WORLD_SIZE="2", LOCAL_RANK="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port - 1),
+                      TLSGPU_RDZV_TOKEN="job-a")
+    from tlslite_amd.shard import ShardGroup
+    g = ShardGroup(timeout=60)
+    q.put(g.sum(2.0))
+    g.close()
+
+
+def test_shard_rendezvous_drops_foreign_peers():
+    """Rank 0 of the shard rendezvous only admits peers that present the job's token
+    (TLSGPU_RDZV_TOKEN): a foreign connection claiming rank 1 with another token and one
+    that sends garbage are dropped, and the real rank 1 still joins."""
+    import struct
+    import time
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p0 = ctx.Process(target=_token_rank0, args=(port, q))
+    p0.start()
+    deadline = time.monotonic() + 60
+    while True:
+        try:
+            s = socket.create_connection(("127.0.0.1", port), timeout=2)
+            break
+        except OSError:
+            assert time.monotonic() < deadline
+            time.sleep(0.05)
+    s.sendall(struct.pack("<IB", 1, 5) + b"job-b")  # wrong token, claims rank 1
+    s2 = socket.create_connection(("127.0.0.1", port), timeout=2)
+    s2.sendall(b"\xff")  # truncated hello
+    s2.close()
+    p1 = ctx.Process(target=_token_rank1, args=(port, q))
+    p1.start()
+    res = sorted([q.get(timeout=120), q.get(timeout=120)])
+    for p in (p0, p1):
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s.close()
+    assert res == [3.0, 3.0]

@@ -131,9 +131,10 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //   TG_AB_MAC_LB_MANY / TG_AB_MAC_PF_MANY  launch bound / prefetch ring of the many-chains MAC kernel
 //   TG_AB_NO_PAIR    cipher phase on the quad layout (cbc_kernel) in the throughput regimes too,
 //                    instead of 2 lanes per chain (cbc_pair_kernel)
-//   TG_AB_SPLIT_PAIR the split prefix / MAC / cbc_pair_kernel path in the pair regime instead of
-//                    seal_fused_kernel (tg_fused.h); TG_AB_FUSED_G / TG_AB_FUSED_GM: the fused
-//                    kernel's prefetch group in the one-generation / many-chains regime
+//   TG_AB_FUSED      the one-kernel seal (seal_fused_kernel, tg_fused.h) in the pair regime instead
+//                    of the split prefix / MAC / cbc_pair_kernel path; TG_AB_FUSED_G / _GM: its
+//                    prefetch group in the one-generation / many-chains regime; TG_AB_FZ_*: its
+//                    MAC waves' priority, gating and lead (tg_fused.h)
 //   TG_AB_PAIR_G1 / TG_AB_PAIR_GM  the pair kernel's prefetch group (blocks) in the one-generation
 //                    (cfg2) / many-chains (cfg3) regime; TG_AB_PAIR_MAC_MANY: the 128-VGPR MAC
 //                    kernel in the one-generation pair regime too
@@ -223,6 +224,33 @@ __device__ __forceinline__ void quad_transpose4(uint32_t x[4], uint32_t q) {
     quad_bfly<0x4E>(x[1], x[3], m1);
 }
 
+// Quad-cooperative chunk load: lane q fetches bytes [16q, 16q+16) of each quad member L's
+// 64-byte chunk at src (member L's own pointer, exchanged over DPP) into nx[L].  Every lane of
+// the quad must execute it; src must point at 64 readable bytes, 16-byte aligned.
+__device__ __forceinline__ void coop_load(const uint8_t* src, uint32_t q, uint4 nx[4]) {
+    const uint32_t lo = (uint32_t)(uintptr_t)src, hi = (uint32_t)((uintptr_t)src >> 32);
+#define TG_QL(L) nx[L] = ldg16((const uint8_t*)(((uint64_t)quad_lane<L>(hi) << 32) | quad_lane<L>(lo)) + 16 * q);
+    TG_QL(0) TG_QL(1) TG_QL(2) TG_QL(3)
+#undef TG_QL
+}
+// The lane's own chunk words out of a coop_load ring slot: four 4x4 quad transposes
+// (component t of lane p's piece of record L = record L's word 4p + t)
+__device__ __forceinline__ void coop_transpose(const uint4 nx[4], uint32_t q, uint32_t d[16]) {
+    uint32_t x[4];
+    x[0] = nx[0].x; x[1] = nx[1].x; x[2] = nx[2].x; x[3] = nx[3].x;
+    quad_transpose4(x, q);
+    d[0] = x[0]; d[4] = x[1]; d[8] = x[2]; d[12] = x[3];
+    x[0] = nx[0].y; x[1] = nx[1].y; x[2] = nx[2].y; x[3] = nx[3].y;
+    quad_transpose4(x, q);
+    d[1] = x[0]; d[5] = x[1]; d[9] = x[2]; d[13] = x[3];
+    x[0] = nx[0].z; x[1] = nx[1].z; x[2] = nx[2].z; x[3] = nx[3].z;
+    quad_transpose4(x, q);
+    d[2] = x[0]; d[6] = x[1]; d[10] = x[2]; d[14] = x[3];
+    x[0] = nx[0].w; x[1] = nx[1].w; x[2] = nx[2].w; x[3] = nx[3].w;
+    quad_transpose4(x, q);
+    d[3] = x[0]; d[7] = x[1]; d[11] = x[2]; d[15] = x[3];
+}
+
 // MAC over the 64-byte chunks of the quad's four records, loaded cooperatively: per load
 // instruction lane q fetches bytes [16q, 16q+16) of record L's chunk, so a quad reads a
 // record's 64 contiguous bytes with one instruction -- a wave touches 16 segments per load
@@ -260,20 +288,8 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
         for (int k = 0; k < PF; k++) {
             const uint32_t c = c0 + k;
             if (c >= nmax) break;
-            // component t of lane p's piece of record L = record L's word 4p + t
-            uint32_t d[16], x[4];
-            x[0] = nxt[k][0].x; x[1] = nxt[k][1].x; x[2] = nxt[k][2].x; x[3] = nxt[k][3].x;
-            quad_transpose4(x, q);
-            d[0] = x[0]; d[4] = x[1]; d[8] = x[2]; d[12] = x[3];
-            x[0] = nxt[k][0].y; x[1] = nxt[k][1].y; x[2] = nxt[k][2].y; x[3] = nxt[k][3].y;
-            quad_transpose4(x, q);
-            d[1] = x[0]; d[5] = x[1]; d[9] = x[2]; d[13] = x[3];
-            x[0] = nxt[k][0].z; x[1] = nxt[k][1].z; x[2] = nxt[k][2].z; x[3] = nxt[k][3].z;
-            quad_transpose4(x, q);
-            d[2] = x[0]; d[6] = x[1]; d[10] = x[2]; d[14] = x[3];
-            x[0] = nxt[k][0].w; x[1] = nxt[k][1].w; x[2] = nxt[k][2].w; x[3] = nxt[k][3].w;
-            quad_transpose4(x, q);
-            d[3] = x[0]; d[7] = x[1]; d[11] = x[2]; d[15] = x[3];
+            uint32_t d[16];
+            coop_transpose(nxt[k], q, d);
             // the ring is reloaded as a whole after its last slot is transposed: a record's
             // consecutive 64-B chunks (whole 128-B lines) are requested back to back rather than
             // one compression apart (cfg2 901-902 -> 916-918 GiB/s with PF = 2)

@@ -54,6 +54,13 @@ constexpr uint32_t FZ_LDS_BYTES = FZ_TAIL + TAIL_SLOT * FZ_SLOTS;
 static_assert(FZ_LDS_BYTES <= 160 * 1024, "gfx950 LDS per workgroup");
 // watchdog: iterations of a wait (each with an s_sleep) before it gives up (~0.5 s)
 constexpr uint32_t FZ_WATCHDOG = 1u << 22;
+// A/B switches (tools/build_ab.sh): TG_AB_FZ_MAC_PRIO  the MAC waves' priority (default: the
+// split path's MAC priority); TG_AB_FZ_NOGATE  MAC loads not gated on the cipher's progress;
+// TG_AB_FZ_NOMAC  timing only (wrong MACs): the MAC lanes hand over their tails without
+// computing them, i.e. the cipher waves' time inside this kernel
+#ifndef TG_AB_FZ_MAC_PRIO
+#define TG_AB_FZ_MAC_PRIO TG_AB_MAC_PRIO
+#endif
 
 __device__ __forceinline__ uint32_t fz_ld(uint32_t addr) {
     return __hip_atomic_load((lds_u32_t*)(size_t)addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -201,91 +208,126 @@ __device__ __forceinline__ void fz_mac(const tlsgpu_chain* __restrict__ chains, 
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
     constexpr uint32_t BS = 16;
-    __builtin_amdgcn_s_setprio(TG_AB_MAC_PRIO);
+    __builtin_amdgcn_s_setprio(TG_AB_FZ_MAC_PRIO);
     const uint32_t slot = ((threadIdx.x >> 6) - FZ_CIPHER_WAVES) * 64 + (threadIdx.x & 63);
     const uint32_t a_loaded = FZ_LOADED + 4 * slot, a_done = FZ_DONE + 4 * slot, a_ready = FZ_READY + 4 * slot;
     uint32_t cid = blockIdx.x * cpw + slot;
     uint32_t phase = (slot < cpw && cid < nchains) ? FZ_NEXT_CHAIN : FZ_IDLE;
     uint32_t base = 0, k = 0;  // the slot's cumulative plaintext bytes / records (as the cipher lanes count)
-    tlsgpu_chain ch = {};
+    uint32_t ch_first = 0, ch_count = 0;  // the current chain's records
     ConnState* st = states;
     bool ok = false;
     uint64_t seq = 0;
     uint32_t E = 0, j = 0, n = 0, nfull = 0, c = 0, ln = 0;
-    tlsgpu_record R = {};
     const uint8_t* P = pt;
     M mac;
-    uint32_t cur[16], nxt[16];
+    // the BULK phase's ring of two quad-cooperative chunk loads (mac_bulk_coop's pattern: lane
+    // q of a quad holds bytes [16q, 16q+16) of each quad member's chunk, one dwordx4 per
+    // member, so a load instruction covers 16 whole 64-B pieces)
+    uint4 ring0[4], ring1[4];
 #pragma unroll
-    for (int i = 0; i < 16; i++) cur[i] = nxt[i] = 0;
-    bool have_cur = false, have_nxt = false;
+    for (int i = 0; i < 4; i++) ring0[i] = ring1[i] = make_uint4(0, 0, 0, 0);
+    bool v0 = false, v1 = false;  // the slot holds this lane's next chunk (slot 0 before slot 1)
+    bool coop = true;             // the record's plaintext is 16-byte aligned (else per-lane loads)
+    const uint32_t q = threadIdx.x & 3u;
     uint32_t idle_iters = 0;
+    // chunk x may be read once the cipher lanes have issued the loads of its bytes (so the
+    // read finds the lines in the L2), or TG_AB_FZ_LEAD bytes before
+#ifndef TG_AB_FZ_LEAD
+#define TG_AB_FZ_LEAD 0
+#endif
+#ifdef TG_AB_FZ_NOGATE
+#define TG_FZ_ALLOWED(x) true
+#else
+#define TG_FZ_ALLOWED(x) fz_ge(fz_ld(a_loaded) + TG_AB_FZ_LEAD, base + 64u * ((x) + 1))
+#endif
     while (__any(phase != FZ_IDLE)) {
         bool progress = false;
-        if (phase == FZ_NEXT_CHAIN) {  // start the slot's next chain (prefix_kernel's header test)
-            ch = chains[cid];
-            st = states + ch.state;
-            uint4 h1;
-            ok = fz_state_ok<CID, MAC, SSL3>(st, h1);
-            seq = (uint64_t)h1.x | ((uint64_t)h1.y << 32);
-            E = h1.z ? BS : 0u;
-            j = 0;
-            phase = FZ_NEXT_REC;
-            progress = true;
-        }
-        if (phase == FZ_NEXT_REC) {
-            const uint32_t r = ch.first + j;
-            if (j >= ch.count || r >= nrecords) {  // chain finished
-                if (ok) st->seqnum = seq;
-                cid += gridDim.x * cpw;
-                phase = cid < nchains ? FZ_NEXT_CHAIN : FZ_IDLE;
-            } else {
-                R = recs[r];
-                n = R.pt_len;
-                uint32_t body;
-                const int32_t stt = seal_record_status<DL, BS>(ok, n, E, R.wire_off, wire_cap, body);
-                if (stt != 1) {
-                    wire_len[r] = stt;
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    fz_st(a_ready, k + 1);
-                    base += n;
-                    k++;
-                    j++;
+        if (__any(phase == FZ_NEXT_CHAIN || phase == FZ_NEXT_REC)) {
+            if (phase == FZ_NEXT_CHAIN) {  // start the slot's next chain (prefix_kernel's header test)
+                const tlsgpu_chain ch = chains[cid];
+                ch_first = ch.first;
+                ch_count = ch.count;
+                st = states + ch.state;
+                uint4 h1;
+                ok = fz_state_ok<CID, MAC, SSL3>(st, h1);
+                seq = (uint64_t)h1.x | ((uint64_t)h1.y << 32);
+                E = h1.z ? BS : 0u;
+                j = 0;
+                phase = FZ_NEXT_REC;
+                progress = true;
+            }
+            if (phase == FZ_NEXT_REC) {
+                const uint32_t r = ch_first + j;
+                if (j >= ch_count || r >= nrecords) {  // chain finished
+                    if (ok) st->seqnum = seq;
+                    cid += gridDim.x * cpw;
+                    phase = cid < nchains ? FZ_NEXT_CHAIN : FZ_IDLE;
                 } else {
-                    P = pt + R.pt_off;
-                    mac.begin(st, seq, R.content_type, n);
-                    nfull = n >> 6;
-                    c = ln = 0;
-                    phase = FZ_BULK;
+                    const tlsgpu_record R = recs[r];
+                    n = R.pt_len;
+                    uint32_t body;
+                    const int32_t stt = seal_record_status<DL, BS>(ok, n, E, R.wire_off, wire_cap, body);
+                    if (stt != 1) {
+                        wire_len[r] = stt;
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                        fz_st(a_ready, k + 1);
+                        base += n;
+                        k++;
+                        j++;
+                    } else {
+                        P = pt + R.pt_off;
+                        coop = ((uintptr_t)P & 15) == 0;
+                        mac.begin(st, seq, R.content_type, n);
+                        nfull = n >> 6;
+                        c = ln = 0;
+                        phase = FZ_BULK;
+#ifdef TG_AB_FZ_NOMAC
+                        c = ln = nfull;
+                        phase = FZ_FIN;
+#endif
+                    }
                 }
+                progress = true;
             }
+        }
+        // slot 0 then slot 1: compress the slot's chunk, refill the slot with chunk ln (the
+        // other slot's compression hides the load); loads and compressions alternate between
+        // the slots in the same order, so chunks are compressed in load order
+#define TG_FZ_RING_STEP(rs, vs)                                                                          \
+        {                                                                                                \
+            if (__any(vs)) {                                                                             \
+                uint32_t d[16];                                                                          \
+                coop_transpose(rs, q, d);                                                                \
+                if (vs) {                                                                                \
+                    mac.update(d);                                                                       \
+                    c++;                                                                                 \
+                    progress = true;                                                                     \
+                }                                                                                        \
+            }                                                                                            \
+            const bool ld = phase == FZ_BULK && coop && ln < nfull && TG_FZ_ALLOWED(ln);                \
+            vs = ld;                                                                                     \
+            if (__any(ld)) {                                                                             \
+                coop_load(ld ? P + 64 * ln : (const uint8_t*)st, q, rs);                                 \
+                progress = true;                                                                         \
+            }                                                                                            \
+            if (ld) ln++;                                                                                \
+        }
+        TG_FZ_RING_STEP(ring0, v0)
+        TG_FZ_RING_STEP(ring1, v1)
+#undef TG_FZ_RING_STEP
+        if (phase == FZ_BULK && !coop && c < nfull && TG_FZ_ALLOWED(c)) {  // unaligned plaintext: per-lane loads
+            uint32_t d[16];
+            load64(P + 64 * c, d);
+            mac.update(d);
+            c++;
+            ln++;
             progress = true;
         }
-        if (phase == FZ_BULK) {
-            // compress the chunk in cur; move the prefetched one in; issue the next load once
-            // the cipher lanes have issued theirs for the same bytes
-            if (have_cur) {
-                mac.update(cur);
-                c++;
-                have_cur = false;
-                progress = true;
-            }
-            if (have_nxt) {
-#pragma unroll
-                for (int i = 0; i < 16; i++) cur[i] = nxt[i];
-                have_cur = true;
-                have_nxt = false;
-            }
-            if (ln < nfull && fz_ge(fz_ld(a_loaded), base + 64u * (ln + 1))) {
-                load64(P + 64 * ln, nxt);
-                ln++;
-                have_nxt = true;
-                progress = true;
-            }
-            if (c == nfull) phase = FZ_FIN;
-        }
+        if (phase == FZ_BULK && c == nfull) phase = FZ_FIN;  // every chunk compressed: the ring is empty
         if (phase == FZ_FIN && fz_ge(fz_ld(a_done), k)) {  // the previous record's tail is consumed
-            const uint32_t r = ch.first + j;
+            const uint32_t r = ch_first + j;
+            const tlsgpu_record R = recs[r];  // reloaded here rather than kept through the bulk
             const uint32_t r64 = n & 63;
             uint32_t tl[16];
             load_partial(P + 64 * nfull, r64, tl);
@@ -352,7 +394,7 @@ __device__ __forceinline__ void fz_mac(const tlsgpu_chain* __restrict__ chains, 
         if (!__any(progress)) {
             __builtin_amdgcn_s_sleep(2);
             if (++idle_iters > FZ_WATCHDOG) {
-                if (phase == FZ_BULK || phase == FZ_FIN) wire_len[ch.first + j] = TLSGPU_EHIP;
+                if (phase == FZ_BULK || phase == FZ_FIN) wire_len[ch_first + j] = TLSGPU_EHIP;
                 break;
             }
         } else {
@@ -360,6 +402,8 @@ __device__ __forceinline__ void fz_mac(const tlsgpu_chain* __restrict__ chains, 
         }
     }
 }
+
+#undef TG_FZ_ALLOWED
 
 // One workgroup per CU (persistent over chain generations), 12 waves: 8 cipher + 4 MAC.
 template <int NR, int MAC, bool SSL3, int G>

@@ -16,7 +16,9 @@
 #include "tg_device.h"
 #include "tg_quad.h"
 #include "tg_aes3.h"
+#ifdef TG_AB_FUSED
 #include "tg_fused.h"
+#endif
 #include "tg_open3.h"
 #include "tg_derive.h"
 #include "tg_launch.h"
@@ -414,14 +416,17 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
     return hipGetLastError();
 }
 
-// The AES seal in one kernel (tg_fused.h) in the pair regime: every CU gets a full
-// 256-chain workgroup (cfg2, cfg3), so the cipher's and the MAC's reads of the plaintext can
-// be one.  TG_AB_SPLIT_PAIR: the split prefix / MAC / cipher kernels there too (A/B builds).
+// TG_AB_FUSED (A/B builds only): the AES seal in one kernel (tg_fused.h) in the pair regime,
+// the cipher's and the MAC's reads of the plaintext one.  Measured slower than the split
+// pipeline (cfg2 870 vs 965 GiB/s, cfg3 469 vs 558, same box), so the product
+// runs the split prefix / MAC / cbc_pair_kernel path there.
 static bool fused_regime(uint32_t nchains, hipStream_t s) {
-#ifdef TG_AB_SPLIT_PAIR
-    return false;
-#else
+#ifdef TG_AB_FUSED
     return pair_regime(nchains, s);
+#else
+    (void)nchains;
+    (void)s;
+    return false;
 #endif
 }
 #ifndef TG_AB_FUSED_G
@@ -431,6 +436,7 @@ static bool fused_regime(uint32_t nchains, hipStream_t s) {
 #define TG_AB_FUSED_GM 8
 #endif
 
+#ifdef TG_AB_FUSED
 template <int NR, int MAC, bool SSL3>
 static hipError_t launch_fused(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
@@ -448,6 +454,13 @@ static hipError_t launch_fused(const tlsgpu_chain* chains, uint32_t nchains, con
                        states, wire_len, cpw, wire_cap);
     return hipGetLastError();
 }
+#else
+template <int NR, int MAC, bool SSL3>
+static hipError_t launch_fused(const tlsgpu_chain*, uint32_t, const tlsgpu_record*, uint32_t, const uint8_t*, uint8_t*,
+                               ConnState*, int32_t*, uint64_t, hipStream_t) {
+    return hipErrorInvalidDeviceFunction;  // never called: fused_regime() is false in the product
+}
+#endif
 
 // phase 2 (stream s2, after phase 1): CBC over [explicit IV | P blocks | tail]
 template <int NR>
