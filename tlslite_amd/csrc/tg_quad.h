@@ -184,51 +184,9 @@ struct PairAes : QuadAes {
     // one block whose two columns are already whitened
     template <int NR>
     __device__ __forceinline__ void encrypt_w(uint32_t& a, uint32_t& b, const uint32_t* ka, const uint32_t* kb) const {
-#ifdef TG_AB_PAIR_PIPE
-        encrypt_pipe<NR>(a, b, ka, kb);
-#else
 #pragma unroll
         for (int r = 1; r < NR; r++) round(a, b, ka[r], kb[r]);
         last(a, b, ka[NR], kb[NR]);
-#endif
-    }
-    // The same rounds with the lookups software-pipelined across them: column a of round r is
-    // formed from the first two of round r's b lookups, so its four lookups for round r + 1
-    // issue while the last two b lookups of round r are still in flight, and round r + 1's b
-    // lookups follow as soon as b is out.  Issue is in order: in round()'s interleaved order a
-    // b lookup second in the round held the following six until b was out.
-    template <int NR>
-    __device__ __forceinline__ void encrypt_pipe(uint32_t& a, uint32_t& b, const uint32_t* ka,
-                                                 const uint32_t* kb) const {
-        uint32_t A2 = look<2, 2>(a), A0 = look<0, 0>(a), A1 = look<1, 1>(a), A3 = look<3, 3>(a);
-        uint32_t B3 = look<3, 3>(b), B1 = look<1, 1>(b), B2 = look<2, 2>(b), B0 = look<0, 0>(b);
-        uint32_t fa0 = 0, fa2 = 0, fa3 = 0, fa1 = 0;
-#pragma unroll
-        for (int r = 1; r < NR; r++) {
-            const uint32_t sa = __builtin_amdgcn_bitop3_b32(A2, B3, ka[r], 0x96);
-            const uint32_t na = (A0 ^ B1) ^ swap(sa);
-            if (r + 1 < NR) {
-                A2 = look<2, 2>(na); A0 = look<0, 0>(na); A1 = look<1, 1>(na); A3 = look<3, 3>(na);
-            } else {  // final round: S-box byte B of s at byte B of table (B+2)&3 (last())
-                fa0 = look<2, 0>(na); fa2 = look<0, 2>(na); fa3 = look<1, 3>(na); fa1 = look<3, 1>(na);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            const uint32_t sb = __builtin_amdgcn_bitop3_b32(A1, B2, kb[r], 0x96);
-            const uint32_t nb = (B0 ^ A3) ^ swap(sb);
-            if (r + 1 < NR) {
-                B3 = look<3, 3>(nb); B1 = look<1, 1>(nb); B2 = look<2, 2>(nb); B0 = look<0, 0>(nb);
-            } else {
-                B1 = look<3, 1>(nb); B3 = look<1, 3>(nb); B0 = look<2, 0>(nb); B2 = look<0, 2>(nb);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // last(): tb1 = B1, tb3 = B3, tb0 = B0, tb2 = B2
-        const uint32_t oa = perm(B1, fa0, 0x0c0c0500u);
-        const uint32_t sa = perm(B3, fa2, 0x07020c0cu) ^ ka[NR];
-        const uint32_t ob = perm(fa3, B0, 0x070c0c00u);
-        const uint32_t sb = perm(B2, fa1, 0x0c06010cu) ^ kb[NR];
-        a = oa ^ swap(sa);
-        b = ob ^ swap(sb);
     }
 };
 

@@ -7,6 +7,9 @@
 //   quad2b  as quad2 with the quad1b XOR order
 //   pair1   2 lanes/chain (2 columns per lane, 8 lookups, one DPP swap),     8 waves/CU
 //   pair2   2 lanes/chain, 2 chains per lane pair,                           4 waves/CU
+//   pairg1  pair1 with the two T3 lookups of a round from a 1 KiB table in global memory
+//           (the vector L1 as a second gather port beside the LDS), 8 waves/CU
+//   pairg2  pair1 with the T3 and T2 lookups (4 of 8) from global tables
 //   lane1   1 lane/chain (16 lookups per lane),                              4 waves/CU
 //   *@512   the same at 512 chains per CU (cfg3 has 4,096 per CU)
 //   latency mode (argv[2] = "lat"): 2 and 16 chains per CU (cfg4 at 8 GPUs / 1 GPU):
@@ -58,6 +61,35 @@ struct QuadAesB : QuadAes {
 };
 
 // 2 lanes per chain: the product's PairAes (tg_quad.h)
+
+// T2 / T3 in global memory (the second gather port): T_t = rotl(T0, 8t) as aes_lds_fill
+__device__ uint32_t g_t[2][256];
+__global__ void fill_gtables() {
+    const uint32_t e = threadIdx.x;
+    const uint32_t v = c_aes.te0[e];
+    g_t[0][e] = (v << 16) | (v >> 16);  // T2
+    g_t[1][e] = (v << 24) | (v >> 8);   // T3
+}
+template <int NG>  // NG = 1: T3 from global; 2: T2 and T3
+struct PairAesG : PairAes {
+    template <int T, int B>
+    __device__ __forceinline__ uint32_t lk(uint32_t s) const {
+        if constexpr ((T == 3 && NG >= 1) || (T == 2 && NG >= 2)) {
+            const uint32_t* g = g_t[T - 2];
+            return g[(s >> (8 * B)) & 0xffu];
+        } else {
+            return look<T, B>(s);
+        }
+    }
+    __device__ __forceinline__ void round(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
+        const uint32_t a2 = lk<2, 2>(a), b3 = lk<3, 3>(b), a1 = lk<1, 1>(a), b2 = lk<2, 2>(b);
+        const uint32_t a0 = lk<0, 0>(a), b1 = lk<1, 1>(b), b0 = lk<0, 0>(b), a3 = lk<3, 3>(a);
+        const uint32_t sa = __builtin_amdgcn_bitop3_b32(a2, b3, ka, 0x96);
+        const uint32_t sb = __builtin_amdgcn_bitop3_b32(a1, b2, kb, 0x96);
+        a = (a0 ^ b1) ^ swap(sa);
+        b = (b0 ^ a3) ^ swap(sb);
+    }
+};
 
 __device__ __forceinline__ void lane_round(const QuadAes& L, uint32_t s[4], const uint32_t* k) {
     uint32_t t[4];
@@ -132,8 +164,8 @@ __global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict_
         }
 #pragma unroll
         for (int i = 0; i < ILP; i++) out[ch[i] * 4 + q] = x[i];
-    } else if constexpr (LAYOUT == 2) {  // pair: lane h = columns 2h, 2h+1
-        PairAes P;
+    } else if constexpr (LAYOUT == 2 || LAYOUT == 7 || LAYOUT == 8) {  // pair: lane h = columns 2h, 2h+1
+        PairAesG<LAYOUT == 7 ? 1 : LAYOUT == 8 ? 2 : 0> P;
         P.init();
         const uint32_t h = lane & 1;
         const uint32_t pr = wave * 32 + (lane >> 1);
@@ -161,7 +193,10 @@ __global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict_
 #pragma unroll
             for (int r = 1; r < NR; r++) {
 #pragma unroll
-                for (int i = 0; i < ILP; i++) P.round(a[i], bb[i], ka[r], kb[r]);
+                for (int i = 0; i < ILP; i++) {
+                    if constexpr (LAYOUT == 2) P.PairAes::round(a[i], bb[i], ka[r], kb[r]);
+                    else P.round(a[i], bb[i], ka[r], kb[r]);
+                }
             }
 #pragma unroll
             for (int i = 0; i < ILP; i++) P.last(a[i], bb[i], ka[NR], kb[NR]);
@@ -226,7 +261,7 @@ static uint32_t* g_side_out = nullptr;
 
 template <int LAYOUT, int ILP, int CPC>
 static Res run(const char* name, const uint32_t* d_ek, int cus, int blocks, int corun = 0) {
-    const int lanes_per_chain = LAYOUT == 6 ? 64 : LAYOUT >= 4 ? 4 : LAYOUT;
+    const int lanes_per_chain = LAYOUT == 6 ? 64 : (LAYOUT == 7 || LAYOUT == 8) ? 2 : LAYOUT >= 4 ? 4 : LAYOUT;
     const int threads = CPC * lanes_per_chain / ILP;
     auto kern = bench_kernel<LAYOUT, ILP, CPC>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -311,6 +346,20 @@ int main(int argc, char** argv) {
         l16.push_back(run<2, 1, 16>("pair1", d_ek, cus, blocks));
         l16.push_back(run<1, 1, 16>("lane1", d_ek, cus, blocks));
         const int bad = compare(l2) | compare(l16);
+        if (!bad) printf("all layouts agree\n");
+        return bad;
+    }
+    hipLaunchKernelGGL(fill_gtables, dim3(1), dim3(256), 0, 0);
+    (void)hipDeviceSynchronize();
+    if (argc > 2 && argv[2][0] == 'g') {  // second gather port: pair with T3 (T2) lookups from global
+        std::vector<Res> g;
+        g.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks));
+        g.push_back(run<7, 1, 256>("pairg1", d_ek, cus, blocks));
+        g.push_back(run<8, 1, 256>("pairg2", d_ek, cus, blocks));
+        g.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks, 2 * blocks));
+        g.push_back(run<7, 1, 256>("pairg1", d_ek, cus, blocks, 2 * blocks));
+        g.push_back(run<8, 1, 256>("pairg2", d_ek, cus, blocks, 2 * blocks));
+        const int bad = compare(g);
         if (!bad) printf("all layouts agree\n");
         return bad;
     }
