@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--share-devices", action="store_true",
                     help="allow --gpus N above the visible device count (ranks share GPUs round-robin)")
+    ap.add_argument("--extra-streams", type=int, default=0,
+                    help="create this many idle HIP streams before the seal pipeline (diagnostic: the pipeline's "
+                         "overlap must survive an application's other streams)")
     ap.add_argument("--dry-run", action="store_true",
                     help="rank plumbing only (no GPU call): every rank reports its RANK / LOCAL_RANK / device, rank 0 "
                          "prints one JSON line; TLSGPU_DRYRUN_DEVICES stands in for the visible device count")
@@ -66,12 +69,17 @@ def parse():
     ap.add_argument("--no-derive", dest="derive", action="store_false",
                     help="skip the batched key-derivation measurement")
     ap.add_argument("--no-open", dest="open", action="store_false", help="skip the open-path measurement")
-    ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false",
+    ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false", default=None,
                     help="skip the PCIe-inclusive measurement (profiling runs)")
+    ap.add_argument("--host-inclusive", dest="host_inclusive", action="store_true",
+                    help="measure the PCIe-inclusive rate (default: cfg2 only -- cfg4's 16 GiB arenas would "
+                         "pin 32 GiB of host memory for it)")
     ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="minimum CPU time of the cpu_baseline sample (the full batch, repeated)")
     a = ap.parse_args()
+    if a.host_inclusive is None:
+        a.host_inclusive = a.config == "cfg2"
     if a.steps is None:
         a.steps = 10 if a.config == "cfg4" else 500
     if a.warmup is None:
@@ -309,6 +317,7 @@ def host_inclusive_rate(wl, chunk=64 << 20, depth=3):
     with HostSealPipeline(chunk, depth) as hp:
         for name, pt_h, wire_h in (("pinned", pin_pt.array[: wl.pt_bytes], pin_wire.array[: wl.wire_bytes]),
                                    ("pageable", pag_pt, pag_wire)):
+            progress("host-inclusive seal, %s arenas" % name)
             best = None
             for _rep in range(3):
                 wl.reset_states()
@@ -572,6 +581,7 @@ def main():
     # ---- warmup + timed region: successive batches through the seal pipeline
     # (per-record MAC phase of batch k+1 overlaps the CBC phase of batch k)
     from tlslite_amd.recordlayer import SealPipeline
+    extra = [Stream() for _ in range(args.extra_streams)]  # noqa: F841 (kept alive through the run)
     pipe = SealPipeline(wl.n_records)
     for _ in range(args.warmup):
         wl.launch(pipeline=pipe)
@@ -697,6 +707,7 @@ def main():
     open_res = None
     if D.world == 1 and args.open:
         try:
+            progress("open leg")
             open_res = open_rate(wl, stream, args.steps)
         except Exception as e:  # reported, never silently replaced
             open_res = {"error": str(e)}
@@ -704,6 +715,7 @@ def main():
     derive_res = None
     if D.world == 1 and args.derive:
         try:
+            progress("derive leg")
             derive_res = derive_rate(stream)
         except Exception as e:  # reported, never silently replaced
             derive_res = {"error": str(e)}

@@ -400,7 +400,18 @@ int tlsgpu_pipeline_create(tlsgpu_pipeline* out, uint32_t max_records) {
     tlsgpu_pipeline p = new tlsgpu_pipeline_s();
     TG_HIP(hipGetDevice(&p->dev));
     TG_HIP(hipStreamCreateWithFlags(&p->mac_s, hipStreamNonBlocking));
-    TG_HIP(hipStreamCreateWithFlags(&p->cbc_s, hipStreamNonBlocking));
+    // The cipher stream at high priority (round 4).  The runtime spreads a process's streams
+    // over a few hardware queues (GPU_MAX_HW_QUEUES, 4 here), kept per priority level, and
+    // the kernels of one queue run in submission order: when the MAC and cipher streams
+    // landed on one queue the phases ran one after the other instead of side by side (one
+    // idle stream created before the pipeline was enough: cfg2 805 instead of 982 GiB/s).
+    // At different priorities they can never share a queue: 981 GiB/s with that extra
+    // stream, 979-980 without (profiles/r04/ab/ab_stream_priority.txt).
+    {
+        int lo_prio = 0, hi_prio = 0;
+        TG_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
+        TG_HIP(hipStreamCreateWithPriority(&p->cbc_s, hipStreamNonBlocking, hi_prio));
+    }
     for (int i = 0; i < PIPE_WS; i++) {
         TG_HIP(hipEventCreateWithFlags(&p->mac_done[i], hipEventDisableTiming));
         TG_HIP(hipEventCreateWithFlags(&p->cbc_done[i], hipEventDisableTiming));
