@@ -40,11 +40,13 @@ constexpr uint32_t TAIL_SLOT = 64;
 #endif
 constexpr int C3_THREADS = 64 * TG_AB_CBC_WAVES;  // 16 cipher waves
 constexpr int C3_CHAINS = 16 * TG_AB_CBC_WAVES;
-// Many-chains regime (more chains than one generation of 16-wave workgroups, cfg3): 12
-// cipher waves per CU and the MAC kernel at <= 128 VGPRs with a one-chunk prefetch, so that
-// two MAC waves fit per SIMD beside three cipher waves (3 x 80 + 2 x 128 <= 512): the MAC
-// phase is that regime's critical path (cfg3 +2 %, same-box A/B; cfg2, one generation,
-// keeps 16 cipher waves: -23 % with 12)
+// Many-chains regime (more chains than one generation of 16-wave workgroups, cfg3): the MAC
+// kernel at <= 128 VGPRs with a one-chunk prefetch.  Beside the pair cipher kernel (8 waves
+// per CU, 89 VGPRs: 2 x 96 allocated per SIMD) two MAC waves per SIMD fit with either MAC
+// form; the two-chunk ring at launch bound 3 (148 VGPRs) measured 1.5 % slower on cfg3 in
+// round 4 (profiles/r04/ab/ab_cfg3_r04.txt).  C3_WAVES_MANY: the quad cipher kernel's waves
+// in this regime (TG_AB_NO_PAIR builds only; 12, so that two MAC waves fit beside them:
+// 3 x 80 + 2 x 128 <= 512)
 #ifndef TG_AB_WAVES_MANY
 #define TG_AB_WAVES_MANY 12
 #endif
