@@ -353,7 +353,7 @@ def open_rate(wl, stream, steps):
     ms = []
     # RC4 / 3DES-only batches (cfg5): the variants open concurrently on two streams, as their
     # seal does; timed by the host clock around both streams (states reset beforehand)
-    conc = None if wl.uses_split_pipeline() else [Stream(), Stream()]
+    conc = None if wl.uses_split_pipeline() else [Stream(high=True), Stream(high=False)]  # separate HW queues
     for _ in range(max(1, min(steps, 20))):
         N.call("tlsgpu_memcpy_d2d", wl.d_ostates.ptr, wl.d_states0.ptr, wl.d_ostates.nbytes, stream.handle)
         if conc:
@@ -594,7 +594,7 @@ def main():
     # RC4 / 3DES-only batches (cfg5) have no phases to overlap: their per-variant seal
     # kernels run concurrently on two streams (disjoint connection states), each step's
     # launch ordered after the previous step's launch of the same variant
-    conc = None if wl.uses_split_pipeline() else [Stream(), Stream()]
+    conc = None if wl.uses_split_pipeline() else [Stream(high=True), Stream(high=False)]  # separate HW queues
     if conc:
         for _ in range(args.warmup):
             wl.launch(conc)

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define TLSGPU_ABI_VERSION 4
+#define TLSGPU_ABI_VERSION 5
 
 /* ---- suite components (tlsrecordlayer.py:1063-1095, constants.py:159-201) */
 enum {
@@ -185,6 +185,12 @@ int tlsgpu_memset(void *dptr, int value, size_t bytes, tlsgpu_stream s);
 
 /* ---- streams / events ---------------------------------------------------- */
 int tlsgpu_stream_create(tlsgpu_stream *s);
+/* ABI 5: a stream at high (high != 0) or normal priority.  The HIP runtime maps a process's
+ * streams onto a few hardware queues per priority level, and kernels of one queue run in
+ * submission order: two streams whose work should overlap are only certain to get separate
+ * queues at different priorities (the seal pipeline's MAC / cipher streams are; DESIGN.md
+ * section 6).  Replaces nothing in the reference (tlslite has no device streams). */
+int tlsgpu_stream_create_priority(tlsgpu_stream *s, int high);
 /* waits for the stream, frees the library-owned seal / open workspaces of this stream
  * (tlsgpu_seal_dev / tlsgpu_open_dev with a NULL workspace), then destroys it */
 int tlsgpu_stream_destroy(tlsgpu_stream s);

@@ -1,5 +1,6 @@
 """GPU parity of the open path (decrypt + padding + MAC verify,
 tlsrecordlayer.py:958-1044) against the CPU oracle and the golden vectors."""
+import os
 import zlib
 
 import numpy as np
@@ -267,3 +268,62 @@ def test_stop_on_alert_like_connection(suite, version):
             assert r.rc4 == o.rc4
         else:
             assert r.iv == o.iv
+
+
+@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES256-SHA256", (3, 3)), ("3DES-SHA", (3, 1)),
+                                           ("AES128-SHA", (3, 0))])
+def test_split_open_parts_like_oracle(suite, version):
+    """The open in parts (launch_open_split: decrypt and padding pass of chain range h+1
+    beside the MAC pass of range h on a second stream; the library does this from 512
+    records per CU per part, TLSGPU_OPEN_PARTS_MIN_RECORDS lowers the threshold here):
+    6,000 connections of 1-6 records of 1-700 B, ~3 % of records tampered or
+    truncated, connection (stop-on-alert) semantics -- every status, plaintext and final
+    state equals the oracle's, across the part boundaries (tlsrecordlayer.py:958-1044)."""
+    from oracle import oracle as O
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import cu_count
+    from tlslite_amd.recordlayer import open_records
+    T = _T()
+    rng = np.random.default_rng(zlib.crc32(repr(("parts", suite, version)).encode()))
+    amap = {0: 0, O.ALERT_BAD_RECORD_MAC: N.ALERT_BAD_RECORD_MAC,
+            O.ALERT_DECRYPTION_FAILED: N.ALERT_DECRYPTION_FAILED}
+    nconn = 6000
+    writers, readers, oreaders, plan = [], [], [], []
+    for ci in range(nconn):
+        mk_t, mk_o = _mk(T, O, suite, version, rng)
+        writers.append(mk_t())
+        readers.append(mk_t())
+        oreaders.append(mk_o())
+        for _ in range(int(rng.integers(1, 7))):
+            plan.append((ci, rng.bytes(int(rng.integers(1, 701))), int(rng.choice([21, 22, 23], p=[0.05, 0.05, 0.9]))))
+    assert len(plan) >= 4 * 16 * cu_count(), "too few records for a part's decrypt to fill the chip"
+    wires = T.seal(writers, plan)
+    recs = []
+    for (ci, _, ct), w in zip(plan, wires):
+        body = bytearray(w[5:])
+        u = rng.random()
+        if u < 0.02:
+            body[int(rng.integers(0, len(body)))] ^= 1 << int(rng.integers(0, 8))
+        elif u < 0.03:
+            body = body[:-1]
+        recs.append((ci, ct, bytes(body)))
+    os.environ["TLSGPU_OPEN_PARTS_MIN_RECORDS"] = "1"
+    try:
+        res = open_records(readers, recs)
+    finally:
+        del os.environ["TLSGPU_OPEN_PARTS_MIN_RECORDS"]
+    stopped = set()
+    for (ci, ct, body), (st, p) in zip(recs, res):
+        if ci in stopped:
+            assert st == N.ALERT_SKIPPED and p is None
+            continue
+        ost, opt = oreaders[ci].open(body, ct)
+        assert st == amap[ost]
+        if ost == 0:
+            assert p == opt
+        else:
+            assert p is None
+            stopped.add(ci)
+    assert stopped, "no alerts exercised"
+    for r, o in zip(readers, oreaders):
+        assert r.seqnum == o.seqnum and r.iv == o.iv

@@ -17,7 +17,7 @@ FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
 OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH = 0, -1, -2, -3, -4, -5
 ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED, ALERT_SKIPPED = -20, -21, -22
 CHAIN_STOP_ON_ALERT = 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 CONN_STATE_BYTES = 2048
 
 
@@ -77,6 +77,7 @@ SIGNATURES = [
     ("tlsgpu_memcpy_d2d", _i, [_vp, _vp, _sz, _vp]),
     ("tlsgpu_memset", _i, [_vp, _i, _sz, _vp]),
     ("tlsgpu_stream_create", _i, [ctypes.POINTER(_vp)]),
+    ("tlsgpu_stream_create_priority", _i, [ctypes.POINTER(_vp), ctypes.c_int]),
     ("tlsgpu_stream_destroy", _i, [_vp]),
     ("tlsgpu_stream_synchronize", _i, [_vp]),
     ("tlsgpu_event_create", _i, [ctypes.POINTER(_vp)]),

@@ -143,6 +143,15 @@ int tlsgpu_stream_create(tlsgpu_stream* s) {
     *s = reinterpret_cast<tlsgpu_stream>(h);
     return 0;
 }
+int tlsgpu_stream_create_priority(tlsgpu_stream* s, int high) {
+    if (!s) return fail(TLSGPU_EINVAL, "null pointer");
+    int least = 0, greatest = 0;
+    TG_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    hipStream_t h;
+    TG_HIP(hipStreamCreateWithPriority(&h, hipStreamNonBlocking, high ? greatest : least));
+    *s = reinterpret_cast<tlsgpu_stream>(h);
+    return 0;
+}
 int tlsgpu_stream_destroy(tlsgpu_stream s) {
     if (!s) return fail(TLSGPU_EINVAL, "the null stream cannot be destroyed");
     TG_HIP(hipStreamSynchronize(HS(s)));

@@ -10,8 +10,10 @@
 // The library has exactly one kernel per (direction, suite variant): no runtime
 // selection between implementations.
 #include <atomic>
+#include <cstdlib>
 #include <mutex>
 #include <set>
+#include <map>
 #include <utility>
 #include "tg_device.h"
 #include "tg_quad.h"
@@ -686,7 +688,46 @@ static bool open_split_variant(uint32_t v) {
 }
 bool open_needs_workspace(uint32_t variant) { return open_split_variant(variant); }
 
-// NR 0 = 3DES (8-byte blocks, open_tdes_kernel)
+// The second stream of a split open (launch_open_split): one per (device, priority), at a
+// priority other than the caller's stream so the two never share a hardware queue (a shared
+// queue runs its kernels in submission order: no overlap), with the events
+// that order the parts.  Enqueueing holds the mutex: calls from several host threads
+// serialise their (microsecond) enqueue, and the events are reused only under it.
+constexpr int OPEN_PARTS = 4;
+struct OpenAux {
+    hipStream_t s2 = nullptr;
+    hipEvent_t dec_done[OPEN_PARTS] = {};
+    hipEvent_t mac_done = nullptr;
+    hipEvent_t pre_done = nullptr;
+};
+static std::mutex open_aux_mu;
+static hipError_t open_aux(hipStream_t s, OpenAux** out) {
+    static std::map<std::pair<int, int>, OpenAux> aux;
+    const int dev = stream_device(s);
+    int least = 0, greatest = 0, p = 0;
+    DeviceGuard guard(dev);
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return e;
+    if ((e = hipStreamGetPriority(s, &p)) != hipSuccess) return e;
+    const int prio = p == greatest ? least : greatest;
+    OpenAux& a = aux[{dev, prio}];
+    if (!a.s2) {
+        if ((e = hipStreamCreateWithPriority(&a.s2, hipStreamNonBlocking, prio)) != hipSuccess) return e;
+        for (auto& ev : a.dec_done)
+            if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&a.mac_done, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventCreateWithFlags(&a.pre_done, hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    *out = &a;
+    return hipSuccess;
+}
+
+// NR 0 = 3DES (8-byte blocks, open_tdes_kernel).  Batches with enough records for every
+// part's decrypt to fill the chip (16 records per CU per part) run in OPEN_PARTS parts by
+// chain range: decrypt + padding pass of part h on the caller's stream, the MAC pass of
+// part h on the second stream once they are done, beside the decrypt of part h+1; the
+// stop pass waits for every MAC.  Smaller batches run every pass once on the caller's
+// stream.
 template <int NR, int MAC, bool SSL3>
 static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* recs,
                                     uint32_t nrecords, const uint8_t* wire, uint8_t* pt, ConnState* states,
@@ -698,24 +739,74 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
     const dim3 gc((nchains + 255) / 256), gr((nrecords + 255) / 256);
     hipLaunchKernelGGL((open_prefix_kernel<CID, MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords,
                        wire, states, status, meta, epoch);
-    if constexpr (NR == 0) {
+    constexpr uint32_t WPB = (NR == 0 ? OT_THREADS : O3_THREADS) / 64;  // records per decrypt workgroup step
+    const uint32_t ncu = cu_count(s);
+    if (NR == 0) {
         if ((e = set_lds(open_tdes_kernel, DES_LDS_BYTES, s)) != hipSuccess) return e;
-        uint32_t grid = (nrecords + (OT_THREADS / 64) - 1) / (OT_THREADS / 64);
-        grid = grid > cu_count(s) ? cu_count(s) : (grid ? grid : 1u);
-        hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire, pt,
-                           states, meta, epoch);
     } else {
-        auto dec = open_aes_kernel<NR == 0 ? 10 : NR>;
-        if ((e = set_lds(dec, AES_DEC_LDS_BYTES, s)) != hipSuccess) return e;
-        uint32_t grid = (nrecords + (O3_THREADS / 64) - 1) / (O3_THREADS / 64);
-        grid = grid > cu_count(s) ? cu_count(s) : (grid ? grid : 1u);
-        hipLaunchKernelGGL(dec, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s, recs, nrecords, wire, pt, states,
-                           meta, epoch);
+        if ((e = set_lds(open_aes_kernel<NR == 0 ? 10 : NR>, AES_DEC_LDS_BYTES, s)) != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords, pt, states,
-                       status, meta, epoch);
-    hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status, meta,
-                       epoch);
+    // the decrypt (persistent: at most one workgroup per CU) + padding pass of chains [c0, c1)
+    auto dec_part = [&](uint32_t c0, uint32_t c1, uint32_t nrec_part, hipStream_t s) {
+        uint32_t grid = (nrec_part + WPB - 1) / WPB;
+        grid = grid > ncu ? ncu : (grid ? grid : 1u);
+        if constexpr (NR == 0)
+            hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire,
+                               pt, states, meta, epoch, c0, c1);
+        else
+            hipLaunchKernelGGL(open_aes_kernel<NR == 0 ? 10 : NR>, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s,
+                               recs, nrecords, wire, pt, states, meta, epoch, c0, c1);
+        hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), dim3((c1 - c0 + 255) / 256), dim3(256), 0, s, chains, nchains,
+                           recs, nrecords, pt, states, status, meta, epoch, c0, c1);
+    };
+#ifdef TG_AB_OPEN_NOSPLIT
+    const bool parts = false;  // A/B: every pass once on the caller's stream
+#else
+    // parts only when each part's MAC pass alone holds two waves per SIMD (one lane per
+    // record): with fewer records a part's MAC takes as long as the whole batch's (its lanes
+    // each hash a whole record), and four of them in a row lose (cfg2: 535-543 vs 733 GiB/s,
+    // cfg5 198 vs 221; cfg3, 1 Mi records: 452 vs 402)
+    // (TLSGPU_OPEN_PARTS_MIN_RECORDS overrides the record threshold: the tests run the split
+    // path on batches of a few thousand records)
+    const char* env = getenv("TLSGPU_OPEN_PARTS_MIN_RECORDS");
+    const uint64_t min_rec = env ? strtoull(env, nullptr, 10) : (uint64_t)OPEN_PARTS * 512u * ncu;
+    const bool parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= min_rec;
+#endif
+    if (!parts) {
+        dec_part(0, nchains, nrecords, s);
+        hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status, meta,
+                           epoch, 0u, nchains);
+    } else {
+        std::lock_guard<std::mutex> g(open_aux_mu);
+        OpenAux* a = nullptr;
+        if ((e = open_aux(s, &a)) != hipSuccess) return e;
+#ifdef TG_AB_OPEN_DEC_AUX
+        // A/B: the decrypt + padding passes on the second stream, the MAC passes on the caller's
+        if ((e = hipEventRecord(a->pre_done, s)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(a->s2, a->pre_done, 0)) != hipSuccess) return e;
+        for (int h = 0; h < OPEN_PARTS; h++) {
+            const uint32_t c0 = (uint32_t)((uint64_t)nchains * h / OPEN_PARTS);
+            const uint32_t c1 = (uint32_t)((uint64_t)nchains * (h + 1) / OPEN_PARTS);
+            dec_part(c0, c1, nrecords / OPEN_PARTS, a->s2);
+            if ((e = hipEventRecord(a->dec_done[h], a->s2)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(s, a->dec_done[h], 0)) != hipSuccess) return e;
+            hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status,
+                               meta, epoch, c0, c1);
+        }
+#else
+        for (int h = 0; h < OPEN_PARTS; h++) {
+            const uint32_t c0 = (uint32_t)((uint64_t)nchains * h / OPEN_PARTS);
+            const uint32_t c1 = (uint32_t)((uint64_t)nchains * (h + 1) / OPEN_PARTS);
+            dec_part(c0, c1, nrecords / OPEN_PARTS, s);
+            if ((e = hipEventRecord(a->dec_done[h], s)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(a->s2, a->dec_done[h], 0)) != hipSuccess) return e;
+            hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, a->s2, recs, nrecords, pt, states,
+                               status, meta, epoch, c0, c1);
+        }
+        if ((e = hipEventRecord(a->mac_done, a->s2)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(s, a->mac_done, 0)) != hipSuccess) return e;
+#endif
+    }
     hipLaunchKernelGGL(open_stop_kernel, gc, dim3(256), 0, s, chains, nchains, recs, nrecords, wire, states, status,
                        meta, epoch);
     return hipGetLastError();

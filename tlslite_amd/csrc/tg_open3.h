@@ -25,6 +25,12 @@
 //                       connection at the alert, :1039-1042).
 //
 // Workspace per record: one 48-byte OpenMeta.
+//
+// A large open runs in parts by chain range (launch_open_split): the decrypt and
+// padding pass of part h+1 on the caller's stream beside the MAC pass of part h on a
+// second stream -- the decrypt is LDS-bound, the MAC VALU-bound.  Each kernel after
+// the prefix takes the part's chain range [c_lo, c_hi) and skips records of other
+// chains (OpenMeta.chain).
 #pragma once
 #include "tg_aes3.h"
 
@@ -38,7 +44,7 @@ struct OpenMeta {
     uint32_t flags;  // OM_*
     uint32_t len;    // plaintext length after explicit-IV removal
     uint32_t n;      // payload length (len - MAC - padding)
-    uint32_t pad;
+    uint32_t chain;  // the record's chain (the part filter of a split open, launch_open_split)
 };
 static_assert(sizeof(OpenMeta) == 48, "OpenMeta");
 constexpr uint32_t OM_DEC = 1, OM_VERIFY = 2, OM_PADOK = 4;
@@ -90,7 +96,7 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
         m.flags = 0;
         m.len = 0;
         m.n = 0;
-        m.pad = 0;
+        m.chain = cid;
         if (!ok) {
             status[r] = TLSGPU_EMISMATCH;
         } else {
@@ -145,11 +151,25 @@ __device__ __forceinline__ void lane_aes_dec(const QuadAesDec& D, uint32_t s[4],
     s[3] = (D.isb<0>(s3) | D.isb<1>(s2) | D.isb<2>(s1) | D.isb<3>(s0)) ^ k[3];
 }
 
+// The records a decrypt wave handles: r0 + i * nwaves for i < 64 (the wave's next 64,
+// in order), those of this launch's part (chains [c_lo, c_hi)) that decrypt.  One lane
+// checks one record's meta, so records of other parts cost no dependent load each.
+__device__ __forceinline__ uint64_t open_dec_batch(const OpenMeta* meta, uint32_t nrecords, uint32_t r0,
+                                                   uint32_t nwaves, uint32_t epoch, uint32_t c_lo, uint32_t c_hi) {
+    const uint32_t rl = r0 + (threadIdx.x & 63) * nwaves;
+    bool mine = false;
+    if (rl < nrecords) {
+        const OpenMeta& m = meta[rl];
+        mine = m.epoch == epoch && (m.flags & OM_DEC) && m.chain - c_lo < c_hi - c_lo;
+    }
+    return __ballot(mine);
+}
+
 template <int NR>
 __global__ void __launch_bounds__(O3_THREADS, 1)
 open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
                 uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
-                uint32_t epoch) {
+                uint32_t epoch, uint32_t c_lo, uint32_t c_hi) {
     aes_lds_fill(nullptr, true);
     __syncthreads();
     QuadAesDec D;
@@ -157,15 +177,25 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (O3_THREADS / 64);
-    for (uint32_t r = blockIdx.x * (O3_THREADS / 64) + wv; r < nrecords; r += nwaves) {
+    for (uint32_t r0 = blockIdx.x * (O3_THREADS / 64) + wv; r0 < nrecords; r0 += 64 * nwaves)
+    for (uint64_t mask = open_dec_batch(meta, nrecords, r0, nwaves, epoch, c_lo, c_hi); mask; mask &= mask - 1) {
+        const uint32_t r = r0 + (uint32_t)__builtin_ctzll(mask) * nwaves;
         const OpenMeta& mt = meta[r];
-        if (mt.epoch != epoch || !(mt.flags & OM_DEC)) continue;
         const ConnState* st = states + mt.state;
         const tlsgpu_open_record R = recs[r];
         const uint32_t E = st->explicit_iv ? 16u : 0u;
         const uint32_t nb = R.ct_len >> 4;
         const uint8_t* C = wire + R.ct_off;
         uint8_t* P = pt + R.pt_off;
+#ifdef TG_AB_OPEN_VKEYS
+        // A/B: the record's round keys copied into VGPRs (a v_bitop3 with an SGPR operand
+        // issues in 4 cycles, with VGPR operands in 2)
+        uint32_t dk[4 * (NR + 1)];
+#pragma unroll
+        for (int i = 0; i < 4 * (NR + 1); i++) asm volatile("v_mov_b32 %0, %1" : "=v"(dk[i]) : "s"(st->dk[i]));
+#else
+        const uint32_t* dk = st->dk;
+#endif
         for (uint32_t b = lane; b < nb; b += 64) {
             uint32_t c[4], p[4];
             load16(C + 16 * b, c);
@@ -175,7 +205,7 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
             } else {
                 load16(C + 16 * (b - 1), p);
             }
-            lane_aes_dec<NR>(D, c, st->dk);
+            lane_aes_dec<NR>(D, c, dk);
 #pragma unroll
             for (int i = 0; i < 4; i++) c[i] ^= p[i];
             if (16 * b >= E) store16(P + 16 * b - E, c);
@@ -243,7 +273,7 @@ struct DesLane {
 __global__ void __launch_bounds__(OT_THREADS, 1)
 open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
                  uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
-                 uint32_t epoch) {
+                 uint32_t epoch, uint32_t c_lo, uint32_t c_hi) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ot_lds[];
     des_lds_fill(ot_lds);  // the kernel's only LDS: the tables start at LDS byte 0
     __syncthreads();
@@ -252,9 +282,10 @@ open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (OT_THREADS / 64);
-    for (uint32_t r = blockIdx.x * (OT_THREADS / 64) + wv; r < nrecords; r += nwaves) {
+    for (uint32_t r0 = blockIdx.x * (OT_THREADS / 64) + wv; r0 < nrecords; r0 += 64 * nwaves)
+    for (uint64_t mask = open_dec_batch(meta, nrecords, r0, nwaves, epoch, c_lo, c_hi); mask; mask &= mask - 1) {
+        const uint32_t r = r0 + (uint32_t)__builtin_ctzll(mask) * nwaves;
         const OpenMeta& mt = meta[r];
-        if (mt.epoch != epoch || !(mt.flags & OM_DEC)) continue;
         const ConnState* st = states + mt.state;
         const uint32_t* ks = &st->des[0][0];
         const tlsgpu_open_record R = recs[r];
@@ -284,10 +315,10 @@ __global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __res
                                                       const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
                                                       const uint8_t* __restrict__ pt, ConnState* __restrict__ states,
                                                       int32_t* __restrict__ status, OpenMeta* __restrict__ meta,
-                                                      uint32_t epoch) {
+                                                      uint32_t epoch, uint32_t c_lo, uint32_t c_hi) {
     constexpr uint32_t DL = Hash<MAC>::DLEN;
-    const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (cid >= nchains) return;
+    const uint32_t cid = c_lo + blockIdx.x * blockDim.x + threadIdx.x;  // chains [c_lo, c_hi) of nchains
+    if (cid >= c_hi || cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
     ConnState* st = states + ch.state;
     uint64_t seq = st->seqnum;
@@ -328,16 +359,54 @@ __global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __res
     if (any) st->seqnum = seq;
 }
 
+// MAC over the plaintext, one lane per record, per-lane 64-B chunk loads with the next chunk
+// prefetched (mac_bulk).  (The seal's quad-cooperative loads, TG_AB_OPEN_MAC_COOP, measured
+// 1-2 % slower here: cfg2 718 vs 733, cfg3 397 vs 402 GiB/s -- with one lane per 16 KiB
+// record the open's MAC is latency-bound, and the transposes sit on that path.)
 template <int MAC, bool SSL3>
 __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
                                                       const uint8_t* __restrict__ pt,
                                                       const ConnState* __restrict__ states,
                                                       int32_t* __restrict__ status,
-                                                      const OpenMeta* __restrict__ meta, uint32_t epoch) {
+                                                      const OpenMeta* __restrict__ meta, uint32_t epoch,
+                                                      uint32_t c_lo, uint32_t c_hi) {
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nrecords) return;
+#ifdef TG_AB_OPEN_MAC_COOP
+    OpenMeta mt = {};
+    // the chain first: records of other parts may be in their padding pass right now
+    bool act = r < nrecords && meta[r].chain - c_lo < c_hi - c_lo;
+    if (act) {
+        mt = meta[r];
+        act = mt.epoch == epoch && (mt.flags & OM_VERIFY);
+    }
+    const ConnState* st = states;
+    tlsgpu_open_record R = {};
+    const uint8_t* P = pt;
+    M mac;
+    const uint32_t n = act ? mt.n : 0u;
+    if (act) {
+        st = states + mt.state;
+        R = recs[r];
+        P = pt + R.pt_off;
+        mac.begin(st, mt.seq, R.content_type, n);
+    }
+    const uint32_t nfull = n >> 6;
+    const bool al16 = ((uintptr_t)P & 15) == 0;
+    uint32_t coop = (act && al16 && nfull) ? 1u : 0u;  // no early exit before: the quad exchanges data
+    coop &= quad_dpp<0xB1>(coop);
+    coop &= quad_dpp<0x4E>(coop);
+    if (coop) {
+        mac_bulk_coop<MAC_PF>(mac, P, nfull, threadIdx.x & 3u);
+    } else if (act) {
+        if (al16) mac_bulk<true>(mac, P, nfull);
+        else mac_bulk<false>(mac, P, nfull);
+    }
+    if (!act) return;
+#else
+    // the chain first: records of other parts may be in their padding pass right now
+    if (r >= nrecords || meta[r].chain - c_lo >= c_hi - c_lo) return;
     const OpenMeta mt = meta[r];
     if (mt.epoch != epoch || !(mt.flags & OM_VERIFY)) return;
     const ConnState* st = states + mt.state;
@@ -349,6 +418,7 @@ __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record*
     const uint32_t nfull = n >> 6;
     if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, P, nfull);
     else mac_bulk<false>(mac, P, nfull);
+#endif
     uint32_t tail[16];
     load_partial(P + 64 * nfull, n & 63, tail);
     uint32_t m[8];

@@ -42,11 +42,17 @@ def arch(ordinal=0):
 
 
 class Stream:
-    def __init__(self, default=False):
+    """A HIP stream of the library (tlsgpu_stream_create); high=True / False: created at
+    high / normal priority (tlsgpu_stream_create_priority) -- two streams whose kernels must
+    overlap are only certain to get separate hardware queues at different priorities."""
+    def __init__(self, default=False, high=None):
         self.handle = ctypes.c_void_p(None)
         self._own = not default
         if not default:
-            N.call("tlsgpu_stream_create", ctypes.byref(self.handle))
+            if high is None:
+                N.call("tlsgpu_stream_create", ctypes.byref(self.handle))
+            else:
+                N.call("tlsgpu_stream_create_priority", ctypes.byref(self.handle), 1 if high else 0)
 
     def synchronize(self):
         N.call("tlsgpu_stream_synchronize", self.handle)

@@ -14,6 +14,8 @@
 #   prof=cfg           rocprofv3 --kernel-trace --stats of a 20-step bench run -> <tag>/prof_<cfg>
 #   pmc=cfg            tools/pmc_kernels.sh (one rocprofv3 --pmc pass per counter group)
 #   ab=cfg:rounds:v1,v2,...   tools/ab_bench.sh (variant "base" = the product library)
+#   openab=cfg:rounds:v1,v2,... the open-path rate (bench's open leg, 20 + 5 seal steps) per
+#                      library build, same call ("base" = the product library)
 #   warm               cfg2 value against warmup / timed step counts
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -103,6 +105,16 @@ import json;d=json.load(open('$O/pmc_$c.json'));k=d['dominant_kernel'];v=d['kern
       IFS=: read c rounds variants <<< "$arg"
       timeout -k 10 1100 bash tools/ab_bench.sh gpurun_out/$TAG/ab_$c $c $rounds ${variants//,/ } \
         || { echo "STEP ab FAILED"; exit 1; } ;;
+    openab)
+      IFS=: read c rounds variants <<< "$arg"
+      for i in $(seq 1 $rounds); do
+        for v in ${variants//,/ }; do
+          if [ $v = base ]; then unset TLSGPU_LIB; else export TLSGPU_LIB=$R/tools/ab/$v/libtlsgpu.so; fi
+          run openab_${c}_${v}_$i 300 python bench.py --config $c --steps 20 --warmup 5 --no-cpu --no-check --no-host-inclusive --no-derive
+          python3 -c "import json;d=json.loads([l for l in open('$O/openab_${c}_${v}_$i.out') if l.startswith('{')][-1]);o=d['open'];print('$c $v open', o['value'], o['ms'], o.get('roundtrip_exact'), 'seal', d['value'])"
+        done
+      done
+      unset TLSGPU_LIB ;;
     warm)
       for ws in "5 20" "5 50" "500 50" "500 500"; do
         set -- $ws
