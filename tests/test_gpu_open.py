@@ -273,9 +273,9 @@ def test_stop_on_alert_like_connection(suite, version):
 @pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES256-SHA256", (3, 3)), ("3DES-SHA", (3, 1)),
                                            ("AES128-SHA", (3, 0))])
 def test_split_open_parts_like_oracle(suite, version):
-    """The open in parts (launch_open_split: decrypt and padding pass of chain range h+1
-    beside the MAC pass of range h on a second stream; the library does this from 512
-    records per CU per part, TLSGPU_OPEN_PARTS_MIN_RECORDS lowers the threshold here):
+    """The open in parts (launch_open_split: decrypt and padding pass of chain range h+1 on
+    a second stream beside the MAC pass of range h; the library does this from 512 records
+    per CU per part, TLSGPU_OPEN_PARTS_MIN_RECORDS lowers the threshold here):
     6,000 connections of 1-6 records of 1-700 B, ~3 % of records tampered or
     truncated, connection (stop-on-alert) semantics -- every status, plaintext and final
     state equals the oracle's, across the part boundaries (tlsrecordlayer.py:958-1044)."""

@@ -696,9 +696,8 @@ bool open_needs_workspace(uint32_t variant) { return open_split_variant(variant)
 constexpr int OPEN_PARTS = 4;
 struct OpenAux {
     hipStream_t s2 = nullptr;
-    hipEvent_t dec_done[OPEN_PARTS] = {};
-    hipEvent_t mac_done = nullptr;
     hipEvent_t pre_done = nullptr;
+    hipEvent_t dec_done[OPEN_PARTS] = {};
 };
 static std::mutex open_aux_mu;
 static hipError_t open_aux(hipStream_t s, OpenAux** out) {
@@ -715,19 +714,17 @@ static hipError_t open_aux(hipStream_t s, OpenAux** out) {
         if ((e = hipStreamCreateWithPriority(&a.s2, hipStreamNonBlocking, prio)) != hipSuccess) return e;
         for (auto& ev : a.dec_done)
             if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
-        if ((e = hipEventCreateWithFlags(&a.mac_done, hipEventDisableTiming)) != hipSuccess) return e;
         if ((e = hipEventCreateWithFlags(&a.pre_done, hipEventDisableTiming)) != hipSuccess) return e;
     }
     *out = &a;
     return hipSuccess;
 }
 
-// NR 0 = 3DES (8-byte blocks, open_tdes_kernel).  Batches with enough records for every
-// part's decrypt to fill the chip (16 records per CU per part) run in OPEN_PARTS parts by
-// chain range: decrypt + padding pass of part h on the caller's stream, the MAC pass of
-// part h on the second stream once they are done, beside the decrypt of part h+1; the
-// stop pass waits for every MAC.  Smaller batches run every pass once on the caller's
-// stream.
+// NR 0 = 3DES (8-byte blocks, open_tdes_kernel).  Large batches of short chains run in
+// OPEN_PARTS parts by chain range: decrypt + padding pass of part h on the second stream,
+// the MAC pass of part h on the caller's stream once they are done, beside the decrypt of
+// part h+1; the stop pass follows the last MAC.  Other batches run every pass once on the
+// caller's stream.
 template <int NR, int MAC, bool SSL3>
 static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* recs,
                                     uint32_t nrecords, const uint8_t* wire, uint8_t* pt, ConnState* states,
@@ -770,7 +767,11 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
     // path on batches of a few thousand records)
     const char* env = getenv("TLSGPU_OPEN_PARTS_MIN_RECORDS");
     const uint64_t min_rec = env ? strtoull(env, nullptr, 10) : (uint64_t)OPEN_PARTS * 512u * ncu;
-    const bool parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= min_rec;
+    // and only for short chains (<= 4 records per chain on average): a part's padding pass
+    // walks each chain's records one dependent load after another, and with long chains
+    // (cfg4: 256 records) four of them in the decrypt stream plus the MAC waves holding the
+    // CUs the next decrypt needs lose (cfg4 587-591 vs 668 GiB/s)
+    const bool parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= min_rec && nrecords <= 4ull * nchains;
 #endif
     if (!parts) {
         dec_part(0, nchains, nrecords, s);
@@ -780,8 +781,10 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
         std::lock_guard<std::mutex> g(open_aux_mu);
         OpenAux* a = nullptr;
         if ((e = open_aux(s, &a)) != hipSuccess) return e;
-#ifdef TG_AB_OPEN_DEC_AUX
-        // A/B: the decrypt + padding passes on the second stream, the MAC passes on the caller's
+        // the decrypt + padding passes on the second stream, the MAC passes on the caller's: the
+        // second stream is the high-priority one whenever the caller's is not, and the decrypt's
+        // workgroups (all of a CU's LDS, 4 waves per SIMD) then get the CUs first as the MAC
+        // waves leave (cfg3 469 vs 454 GiB/s with the MAC passes on the second stream)
         if ((e = hipEventRecord(a->pre_done, s)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(a->s2, a->pre_done, 0)) != hipSuccess) return e;
         for (int h = 0; h < OPEN_PARTS; h++) {
@@ -793,19 +796,6 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
             hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status,
                                meta, epoch, c0, c1);
         }
-#else
-        for (int h = 0; h < OPEN_PARTS; h++) {
-            const uint32_t c0 = (uint32_t)((uint64_t)nchains * h / OPEN_PARTS);
-            const uint32_t c1 = (uint32_t)((uint64_t)nchains * (h + 1) / OPEN_PARTS);
-            dec_part(c0, c1, nrecords / OPEN_PARTS, s);
-            if ((e = hipEventRecord(a->dec_done[h], s)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(a->s2, a->dec_done[h], 0)) != hipSuccess) return e;
-            hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, a->s2, recs, nrecords, pt, states,
-                               status, meta, epoch, c0, c1);
-        }
-        if ((e = hipEventRecord(a->mac_done, a->s2)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(s, a->mac_done, 0)) != hipSuccess) return e;
-#endif
     }
     hipLaunchKernelGGL(open_stop_kernel, gc, dim3(256), 0, s, chains, nchains, recs, nrecords, wire, states, status,
                        meta, epoch);
