@@ -137,8 +137,6 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
 //                    of the split prefix / MAC / cbc_pair_kernel path; TG_AB_FUSED_G / _GM: its
 //                    prefetch group in the one-generation / many-chains regime; TG_AB_FZ_*: its
 //                    MAC waves' priority, gating and lead (tg_fused.h)
-//   TG_AB_OPEN_MAC_COOP open_mac_kernel with the seal's quad-cooperative plaintext loads
-//   TG_AB_OPEN_VKEYS    open_aes_kernel with the record's round keys in VGPRs
 //   TG_AB_OPEN_NOSPLIT  the open path's passes once on the caller's stream (no parts beside
 //                    a second stream, launch_open_split)
 //   TG_AB_PAIR_G1 / TG_AB_PAIR_GM  the pair kernel's prefetch group (blocks) in the one-generation

@@ -187,15 +187,7 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
         const uint32_t nb = R.ct_len >> 4;
         const uint8_t* C = wire + R.ct_off;
         uint8_t* P = pt + R.pt_off;
-#ifdef TG_AB_OPEN_VKEYS
-        // A/B: the record's round keys copied into VGPRs (a v_bitop3 with an SGPR operand
-        // issues in 4 cycles, with VGPR operands in 2)
-        uint32_t dk[4 * (NR + 1)];
-#pragma unroll
-        for (int i = 0; i < 4 * (NR + 1); i++) asm volatile("v_mov_b32 %0, %1" : "=v"(dk[i]) : "s"(st->dk[i]));
-#else
-        const uint32_t* dk = st->dk;
-#endif
+        const uint32_t* dk = st->dk;  // wave-uniform: scalar loads (in VGPRs measured 3 % slower)
         for (uint32_t b = lane; b < nb; b += 64) {
             uint32_t c[4], p[4];
             load16(C + 16 * b, c);
@@ -360,9 +352,10 @@ __global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __res
 }
 
 // MAC over the plaintext, one lane per record, per-lane 64-B chunk loads with the next chunk
-// prefetched (mac_bulk).  (The seal's quad-cooperative loads, TG_AB_OPEN_MAC_COOP, measured
-// 1-2 % slower here: cfg2 718 vs 733, cfg3 397 vs 402 GiB/s -- with one lane per 16 KiB
-// record the open's MAC is latency-bound, and the transposes sit on that path.)
+// prefetched (mac_bulk).  (The seal's quad-cooperative loads measured 1-2 % slower here,
+// round 4: cfg2 718 vs 733, cfg3 397 vs 402 GiB/s -- with one lane per 16 KiB record the
+// open's MAC is latency-bound, and the transposes sit on that path;
+// profiles/r04/ab/ab_open_r04.txt.)
 template <int MAC, bool SSL3>
 __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
                                                       const uint8_t* __restrict__ pt,
@@ -373,38 +366,6 @@ __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record*
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-#ifdef TG_AB_OPEN_MAC_COOP
-    OpenMeta mt = {};
-    // the chain first: records of other parts may be in their padding pass right now
-    bool act = r < nrecords && meta[r].chain - c_lo < c_hi - c_lo;
-    if (act) {
-        mt = meta[r];
-        act = mt.epoch == epoch && (mt.flags & OM_VERIFY);
-    }
-    const ConnState* st = states;
-    tlsgpu_open_record R = {};
-    const uint8_t* P = pt;
-    M mac;
-    const uint32_t n = act ? mt.n : 0u;
-    if (act) {
-        st = states + mt.state;
-        R = recs[r];
-        P = pt + R.pt_off;
-        mac.begin(st, mt.seq, R.content_type, n);
-    }
-    const uint32_t nfull = n >> 6;
-    const bool al16 = ((uintptr_t)P & 15) == 0;
-    uint32_t coop = (act && al16 && nfull) ? 1u : 0u;  // no early exit before: the quad exchanges data
-    coop &= quad_dpp<0xB1>(coop);
-    coop &= quad_dpp<0x4E>(coop);
-    if (coop) {
-        mac_bulk_coop<MAC_PF>(mac, P, nfull, threadIdx.x & 3u);
-    } else if (act) {
-        if (al16) mac_bulk<true>(mac, P, nfull);
-        else mac_bulk<false>(mac, P, nfull);
-    }
-    if (!act) return;
-#else
     // the chain first: records of other parts may be in their padding pass right now
     if (r >= nrecords || meta[r].chain - c_lo >= c_hi - c_lo) return;
     const OpenMeta mt = meta[r];
@@ -418,7 +379,6 @@ __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record*
     const uint32_t nfull = n >> 6;
     if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, P, nfull);
     else mac_bulk<false>(mac, P, nfull);
-#endif
     uint32_t tail[16];
     load_partial(P + 64 * nfull, n & 63, tail);
     uint32_t m[8];
