@@ -148,6 +148,9 @@ struct PairAes : QuadAes {
     __device__ __forceinline__ void round(uint32_t& a, uint32_t& b, uint32_t ka, uint32_t kb) const {
         const uint32_t a2 = look<2, 2>(a), b3 = look<3, 3>(b), a1 = look<1, 1>(a), b2 = look<2, 2>(b);
         const uint32_t a0 = look<0, 0>(a), b1 = look<1, 1>(b), b0 = look<0, 0>(b), a3 = look<3, 3>(a);
+        // (the compiler builds all eight addresses, then issues the eight reads; forcing each
+        // read right after its address op measured 11 % slower, cfg2 864 vs 973 GiB/s, round 4:
+        // profiles/r04/ab/ab_pair_r04.txt)
         const uint32_t sa = __builtin_amdgcn_bitop3_b32(a2, b3, ka, 0x96);  // partner's column 2h+2
         const uint32_t sb = __builtin_amdgcn_bitop3_b32(a1, b2, kb, 0x96);  // partner's column 2h+3
         // (the partner's terms moved by v_mov_dpp ahead of the last lookups and one 3-input XOR
