@@ -11,6 +11,8 @@
 //           (the vector L1 as a second gather port beside the LDS), 8 waves/CU
 //   pairg2  pair1 with the T3 and T2 lookups (4 of 8) from global tables
 //   lane1   1 lane/chain (16 lookups per lane),                              4 waves/CU
+//   mixN    (argv[2] = "m") 32 N chains on N pair waves, the rest on quad waves (N = 4: half and
+//           half, 12 waves/CU)
 //   *@512   the same at 512 chains per CU (cfg3 has 4,096 per CU)
 //   latency mode (argv[2] = "lat"): 2 and 16 chains per CU (cfg4 at 8 GPUs / 1 GPU):
 //   the round is then one chain's dependent latency, reported in shader cycles;
@@ -125,7 +127,48 @@ __global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict_
     __builtin_amdgcn_s_setprio(1);  // as cbc_kernel: win issue arbitration over the MAC waves
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if constexpr (LAYOUT == 4 || LAYOUT == 5 || LAYOUT == 6) {  // quad: lane q = column q
+    if constexpr (LAYOUT == 9) {  // mix: chains [0, 32 PW) on PW pair waves, the rest on quad waves
+        constexpr uint32_t PW = ILP;  // (ILP carries the pair-wave count for this layout)
+        if (wave < PW) {
+            PairAes P;
+            P.init();
+            const uint32_t h = lane & 1;
+            const uint32_t ch = blockIdx.x * CPC + wave * 32 + (lane >> 1);
+            const uint32_t ca = 2 * h, pa = 2 * (1 - h);
+            const uint32_t kwa = ek[ca], kwb = ek[ca + 1];
+            uint32_t ka[NR + 1], kb[NR + 1];
+#pragma unroll
+            for (int r = 1; r <= NR; r++) {
+                ka[r] = ek[4 * r + pa];
+                kb[r] = ek[4 * r + pa + 1];
+            }
+            uint32_t a = init_word(ch, ca), bb = init_word(ch, ca + 1);
+            for (int b = 0; b < blocks; b++) {
+                a ^= kwa;
+                bb ^= kwb;
+#pragma unroll
+                for (int r = 1; r < NR; r++) P.round(a, bb, ka[r], kb[r]);
+                P.last(a, bb, ka[NR], kb[NR]);
+            }
+            out[ch * 4 + ca] = a;
+            out[ch * 4 + ca + 1] = bb;
+        } else {
+            QuadAes L;
+            L.init();
+            const uint32_t q = lane & 3;
+            const uint32_t ch = blockIdx.x * CPC + 32 * PW + (wave - PW) * 16 + (lane >> 2);
+            uint32_t k[NR + 1];
+            QuadAes::round_keys<NR>(ek, q, k);
+            uint32_t x = init_word(ch, q);
+            for (int b = 0; b < blocks; b++) {
+                x ^= k[0];
+#pragma unroll
+                for (int r = 1; r < NR; r++) x = L.template round<false>(x, k[r]);
+                x = L.template last<false>(x, k[NR]);
+            }
+            out[ch * 4 + q] = x;
+        }
+    } else if constexpr (LAYOUT == 4 || LAYOUT == 5 || LAYOUT == 6) {  // quad: lane q = column q
         QuadAesB L;
         L.init();
         const uint32_t q = lane & 3;
@@ -262,7 +305,7 @@ static uint32_t* g_side_out = nullptr;
 template <int LAYOUT, int ILP, int CPC>
 static Res run(const char* name, const uint32_t* d_ek, int cus, int blocks, int corun = 0) {
     const int lanes_per_chain = LAYOUT == 6 ? 64 : (LAYOUT == 7 || LAYOUT == 8) ? 2 : LAYOUT >= 4 ? 4 : LAYOUT;
-    const int threads = CPC * lanes_per_chain / ILP;
+    const int threads = LAYOUT == 9 ? 4 * CPC - 64 * ILP : CPC * lanes_per_chain / ILP;
     auto kern = bench_kernel<LAYOUT, ILP, CPC>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               AES_LDS_BYTES);
@@ -351,6 +394,23 @@ int main(int argc, char** argv) {
     }
     hipLaunchKernelGGL(fill_gtables, dim3(1), dim3(256), 0, 0);
     (void)hipDeviceSynchronize();
+    if (argc > 2 && argv[2][0] == 'm') {  // mixed layout: half the chains on pair waves, half on quad waves
+        std::vector<Res> m;
+        m.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks));
+        m.push_back(run<4, 1, 256>("quad1", d_ek, cus, blocks));
+        m.push_back(run<9, 2, 256>("mix2", d_ek, cus, blocks));
+        m.push_back(run<9, 3, 256>("mix3", d_ek, cus, blocks));
+        m.push_back(run<9, 4, 256>("mix4", d_ek, cus, blocks));
+        m.push_back(run<9, 5, 256>("mix5", d_ek, cus, blocks));
+        m.push_back(run<9, 6, 256>("mix6", d_ek, cus, blocks));
+        m.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks, 2 * blocks));
+        m.push_back(run<9, 3, 256>("mix3", d_ek, cus, blocks, 2 * blocks));
+        m.push_back(run<9, 4, 256>("mix4", d_ek, cus, blocks, 2 * blocks));
+        m.push_back(run<9, 5, 256>("mix5", d_ek, cus, blocks, 2 * blocks));
+        const int bad = compare(m);
+        if (!bad) printf("all layouts agree\n");
+        return bad;
+    }
     if (argc > 2 && argv[2][0] == 'g') {  // second gather port: pair with T3 (T2) lookups from global
         std::vector<Res> g;
         g.push_back(run<2, 1, 256>("pair1", d_ek, cus, blocks));
