@@ -1,0 +1,66 @@
+"""bench.py's parity checkers on the CPU (no GPU): `oracle_check` (the `bit_exact` field) and
+`oracle_timed_check` (`timed_oracle_exact`: the last of n successive seals, states carried)
+accept an output equal to the oracle's and reject one changed byte or one wrong length, on
+small batches of every BASELINE config's shape (tlsrecordlayer.py:538-617: the chain's CBC
+residue / RC4 state and seqnum carry from seal to seal).  Test infrastructure only."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SHAPES = [("cfg2", {"n": 48, "pt_len": 1500}), ("cfg3", {"n": 64, "pt_len": 1434}),
+          ("cfg4", {"nconn": 8, "recs_per_conn": 3, "pt_len": 3000}), ("cfg5", {"n": 40, "pt_len": 2000})]
+
+
+def _sealed(wl, n_launches):
+    """The wire arena and wire lengths after n_launches successive seals (the oracle)."""
+    import bench
+    from oracle import oracle as O
+    protos = bench.oracle_protos(wl, np.arange(wl.n_chains))
+    pt = wl.host_plaintext(O.fill_pattern)
+    wire = np.zeros(wl.wire_bytes, dtype=np.uint8)
+    lens = None
+    for _ in range(n_launches):
+        lens = O.seal_batch(protos, wl.chain_first, wl.chain_count, pt, wl.pt_off, wl.pt_len, wire, wl.wire_off,
+                            nthreads=2, update=True)
+    return wire, np.asarray(lens, dtype=np.int32)
+
+
+def _record_byte(wl, r):
+    return int(wl.wire_off[r]) + 5 + int(wl.wire_len[r] - 5) // 2
+
+
+@pytest.mark.parametrize("name,kw", SHAPES)
+def test_timed_check_accepts_oracle_and_rejects_changes(name, kw):
+    import bench
+    from tlslite_amd import workloads as W
+    wl = W.CONFIGS[name](**kw)
+    wire, lens = _sealed(wl, 3)
+    ok, k = bench.oracle_timed_check(wl, wire, lens, 3, 2)
+    assert ok and k == wl.n_chains  # a small batch: every chain sampled
+    bad = wire.copy()
+    bad[_record_byte(wl, wl.n_records // 2)] ^= 0x40
+    assert not bench.oracle_timed_check(wl, bad, lens, 3, 2)[0]
+    bad_len = lens.copy()
+    bad_len[wl.n_records - 1] += 16
+    assert not bench.oracle_timed_check(wl, wire, bad_len, 3, 2)[0]
+    # the output of two seals is not the output of three (states carried: new IV / keystream / seqnum)
+    wire2, lens2 = _sealed(wl, 2)
+    assert not bench.oracle_timed_check(wl, wire2, lens2, 3, 2)[0]
+
+
+@pytest.mark.parametrize("name,kw", SHAPES)
+def test_oracle_check_accepts_oracle_and_rejects_a_change(name, kw):
+    import bench
+    from tlslite_amd import workloads as W
+    wl = W.CONFIGS[name](**kw)
+    wire, _ = _sealed(wl, 1)
+    ok, _, nrec, nbytes, _, reps = bench.oracle_check(wl, wire, 2)
+    assert ok and nrec == wl.n_records and reps == 1 and nbytes == int(wl.pt_len.sum())
+    bad = wire.copy()
+    bad[_record_byte(wl, 0)] ^= 1
+    assert not bench.oracle_check(wl, bad, 2)[0]
