@@ -227,6 +227,28 @@ def oracle_check(wl, wire_gpu, nthreads, sample=None, min_seconds=0.0):
     return ok, dt, len(recs), int(wl.pt_len[recs].sum()) * reps, nthreads, reps
 
 
+def pmc_traffic(path, workload, n_records, dominant):
+    """(HBM bytes per launch of the dominant kernel, HBM bytes of one seal call) from a PMC
+    summary (tools/pmc_kernels.sh -> profiles/pmc_<cfg>.json), only when it names this kernel
+    and was collected on this very workload (name and record count: a PMC run of another
+    batch size must not price this one); (None, None) otherwise."""
+    if not os.path.exists(path):
+        return None, None
+    try:
+        pj = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+
+    # kernel stems compared up to the first template argument (cbc_kernel<10> is the same
+    # kernel as cbc_kernel<10, false>: the second argument is the round's form)
+    def _key(k):
+        return (k or "").split(",")[0].rstrip(">")
+    if (_key(pj.get("dominant_kernel")) == _key(dominant) and pj.get("workload") == workload
+            and pj.get("records") == n_records):
+        return pj.get("hbm_bytes_per_launch"), pj.get("seal_call_hbm_bytes")
+    return None, None
+
+
 PCIE_GBS = 63.0  # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s per direction (spec)
 
 
@@ -675,22 +697,8 @@ def main():
     # HBM bytes per launch of the same kernel from the committed PMC summary
     # (tools/pmc_kernels.sh -> profiles/pmc_<cfg>.json), only when it names this kernel and
     # was collected on this workload; otherwise traffic is null
-    traffic = seal_call_bytes = None
     tpath = args.traffic or os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
-    if os.path.exists(tpath):
-        try:
-            pj = json.load(open(tpath))
-            # kernel stems compared up to the first template argument (cbc_kernel<10> is the
-            # same kernel as cbc_kernel<10, false>: the second argument is the round's form)
-            def _key(k):
-                return (k or "").split(",")[0].rstrip(">")
-            # ... and only when the PMC run sealed this very workload (name, record count)
-            if (_key(pj.get("dominant_kernel")) == _key(wl.dominant_kernel())
-                    and pj.get("workload") == wl.name and pj.get("records") == wl.n_records):
-                traffic = pj.get("hbm_bytes_per_launch")
-                seal_call_bytes = pj.get("seal_call_hbm_bytes")
-        except Exception:
-            traffic = seal_call_bytes = None
+    traffic, seal_call_bytes = pmc_traffic(tpath, wl.name, wl.n_records, wl.dominant_kernel())
     state_bytes = wl.cipher_state_bytes()
     lookups = wl.aes_lookups() if wl.dominant_kernel().startswith(("cbc_kernel", "cbc_pair_kernel", "seal_fused_kernel")) else None
     lds = None

@@ -64,3 +64,24 @@ def test_oracle_check_accepts_oracle_and_rejects_a_change(name, kw):
     bad = wire.copy()
     bad[_record_byte(wl, 0)] ^= 1
     assert not bench.oracle_check(wl, bad, 2)[0]
+
+
+def test_pmc_traffic_attached_only_to_the_same_workload(tmp_path):
+    """bench.py prices roofline.traffic from a committed PMC summary only when the summary
+    names the run's dominant kernel and was collected on the same workload and record count
+    (a 4,096-connection PMC file once priced a 512-connection run at 8.1x)."""
+    import json
+    import bench
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"dominant_kernel": "cbc_kernel<10, true, 16>", "workload": "cfg4: 4096 conns",
+                             "records": 1048576, "hbm_bytes_per_launch": 123, "seal_call_hbm_bytes": 456}))
+    assert bench.pmc_traffic(str(p), "cfg4: 4096 conns", 1048576, "cbc_kernel<10, false>") == (123, 456)
+    assert bench.pmc_traffic(str(p), "cfg4: 512 conns", 131072, "cbc_kernel<10, true>") == (None, None)
+    assert bench.pmc_traffic(str(p), "cfg4: 4096 conns", 1048576, "cbc_pair_kernel<10, 8, 8>") == (None, None)
+    assert bench.pmc_traffic(str(tmp_path / "missing.json"), "x", 1, "k") == (None, None)
+    (tmp_path / "bad.json").write_text("{not json")
+    assert bench.pmc_traffic(str(tmp_path / "bad.json"), "x", 1, "k") == (None, None)
+    # the committed summaries name their workload and record count
+    for cfg in ("cfg2", "cfg3", "cfg4", "cfg5"):
+        pj = json.load(open(os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg)))
+        assert pj["workload"].startswith(cfg) and pj["records"] > 0 and pj["hbm_bytes_per_launch"] > 0
