@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--no-derive", dest="derive", action="store_false",
                     help="skip the batched key-derivation measurement")
     ap.add_argument("--no-open", dest="open", action="store_false", help="skip the open-path measurement")
+    ap.add_argument("--open", dest="open", action="store_true", help="measure the open path (the default; after a "
+                    "--no-open, e.g. in tools/pmc_kernels.sh's fixed arguments, turns it back on)")
     ap.add_argument("--no-host-inclusive", dest="host_inclusive", action="store_false", default=None,
                     help="skip the PCIe-inclusive measurement (profiling runs)")
     ap.add_argument("--host-inclusive", dest="host_inclusive", action="store_true",
@@ -700,7 +702,7 @@ def main():
     tpath = args.traffic or os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)
     traffic, seal_call_bytes = pmc_traffic(tpath, wl.name, wl.n_records, wl.dominant_kernel())
     state_bytes = wl.cipher_state_bytes()
-    lookups = wl.aes_lookups() if wl.dominant_kernel().startswith(("cbc_kernel", "cbc_pair_kernel", "seal_fused_kernel")) else None
+    lookups = wl.aes_lookups() if wl.dominant_kernel().startswith(("cbc_kernel", "cbc_pair_kernel")) else None
     lds = None
     if lookups:
         g = lookups / (avg_ms / 1e3) / 1e9

@@ -36,6 +36,15 @@
  * Conventions: every function returns 0 on success or a negative error code
  * (TLSGPU_E*).  "_dev" functions take DEVICE pointers and are asynchronous on
  * the given stream (NULL = the default stream of the current device).
+ *
+ * Bounds (ABI 6): the batch seal / open calls take the byte size of each arena and
+ * the number of connection states.  The descriptors live in device memory, so they
+ * are checked on the device, per record: a record whose plaintext or wire range leaves
+ * its arena, or any record of a chain whose state index is >= nstates, gets
+ * TLSGPU_EINVAL in wire_len / status -- nothing of it is read or written, its state is
+ * not touched and no seqnum is consumed (the reference refuses bad lengths at the object
+ * boundary: utils/aes.py:28-34, codec.py:19-20).  Records of a chain past nrecords are
+ * ignored.
  */
 #ifndef TLSGPU_H
 #define TLSGPU_H
@@ -47,7 +56,7 @@
 extern "C" {
 #endif
 
-#define TLSGPU_ABI_VERSION 5
+#define TLSGPU_ABI_VERSION 6
 
 /* ---- suite components (tlsrecordlayer.py:1063-1095, constants.py:159-201) */
 enum {
@@ -191,6 +200,9 @@ int tlsgpu_stream_create(tlsgpu_stream *s);
  * queues at different priorities (the seal pipeline's MAC / cipher streams are; DESIGN.md
  * section 6).  Replaces nothing in the reference (tlslite has no device streams). */
 int tlsgpu_stream_create_priority(tlsgpu_stream *s, int high);
+/* (high == 0 gives the runtime's LEAST priority level -- hipDeviceGetStreamPriorityRange's
+ * "least", below the normal level of tlsgpu_stream_create streams -- so a high / low pair
+ * never shares a hardware queue with each other.) */
 /* waits for the stream, frees the library-owned seal / open workspaces of this stream
  * (tlsgpu_seal_dev / tlsgpu_open_dev with a NULL workspace), then destroys it */
 int tlsgpu_stream_destroy(tlsgpu_stream s);
@@ -242,14 +254,19 @@ size_t tlsgpu_seal_workspace_bytes(uint32_t nrecords);
 int tlsgpu_release_workspaces(void);
 /* number of library-owned workspaces currently allocated (diagnostics / tests) */
 size_t tlsgpu_owned_workspace_count(void);
+/* ABI 6: number of library-owned streams (the split open's second streams, one per device and
+ * priority in use, with their events); tlsgpu_release_workspaces destroys them too */
+size_t tlsgpu_owned_stream_count(void);
 /* Name of the cipher-phase kernel a seal call of `nchains` chains of `variant` runs on the
  * current device (its rocprofv3 name stem, e.g. "cbc_kernel<10, false>"): the layout is
  * chosen from the chains per CU.  Diagnostics / profiling only. */
 int tlsgpu_seal_cipher_kernel(uint32_t variant, uint32_t nchains, char *name, size_t cap);
+/* pt: plaintext arena of pt_bytes, wire: wire arena of wire_bytes, states: nstates states
+ * (ABI 6 bounds, see the top of this file) */
 int tlsgpu_seal_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_record *records,
-                    uint32_t nrecords, const uint8_t *pt, uint8_t *wire, tlsgpu_conn_state *states,
-                    int32_t *wire_len, uint32_t variant, void *workspace, size_t workspace_bytes,
-                    tlsgpu_stream s);
+                    uint32_t nrecords, const uint8_t *pt, size_t pt_bytes, uint8_t *wire, size_t wire_bytes,
+                    tlsgpu_conn_state *states, uint32_t nstates, int32_t *wire_len, uint32_t variant,
+                    void *workspace, size_t workspace_bytes, tlsgpu_stream s);
 /* ---- seal pipeline: successive tlsgpu_pipeline_seal calls overlap the MAC
  * phase of call k+1 with the cipher phase of call k (AES suites; two
  * library-owned streams, three workspaces in rotation, so the MAC phase may run
@@ -261,9 +278,9 @@ int tlsgpu_pipeline_create(tlsgpu_pipeline *p, uint32_t max_records);
 int tlsgpu_pipeline_destroy(tlsgpu_pipeline p);
 int tlsgpu_pipeline_synchronize(tlsgpu_pipeline p);
 int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain *chains, uint32_t nchains,
-                         const tlsgpu_record *records, uint32_t nrecords, const uint8_t *pt, uint8_t *wire,
-                         tlsgpu_conn_state *states, int32_t *wire_len, uint32_t variant,
-                         tlsgpu_event cipher_start, tlsgpu_event cipher_stop);
+                         const tlsgpu_record *records, uint32_t nrecords, const uint8_t *pt, size_t pt_bytes,
+                         uint8_t *wire, size_t wire_bytes, tlsgpu_conn_state *states, uint32_t nstates,
+                         int32_t *wire_len, uint32_t variant, tlsgpu_event cipher_start, tlsgpu_event cipher_stop);
 
 /* ---- host-buffer seal pipeline: records start and end in host socket buffers
  * (tlsrecordlayer.py:616-620 writes each sealed record to the socket).  One call
@@ -284,7 +301,8 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain *chains, uint32_t
  * padding): an RC4 record that would not fit fails the call with TLSGPU_EINVAL; a CBC
  * record (whose size depends on the state's version) gets wire_len = TLSGPU_EINVAL and is
  * not sealed (no seqnum consumed).  Bytes of wire_host between records are written as
- * zeros.
+ * zeros.  A chain whose state index is >= nstates fails the call with TLSGPU_EINVAL (the
+ * chains are host memory here, checked before anything is enqueued).
  * wire_len_host: nrecords int32 (as tlsgpu_seal_dev's wire_len). */
 typedef struct tlsgpu_host_pipeline_s *tlsgpu_host_pipeline;
 int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline *p, size_t chunk_bytes, int depth);
@@ -292,7 +310,7 @@ int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p);
 int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain *chains, uint32_t nchains,
                               const tlsgpu_record *records, uint32_t nrecords, const uint8_t *pt_host,
                               size_t pt_bytes, uint8_t *wire_host, size_t wire_bytes, tlsgpu_conn_state *states,
-                              int32_t *wire_len_host, uint32_t variant);
+                              uint32_t nstates, int32_t *wire_len_host, uint32_t variant);
 
 /* Batch open: status[r] = plaintext length, or TLSGPU_ALERT_* (records 0..nrecords-1;
  * a chain's records open in order on its state, as successive _decryptRecord calls).
@@ -301,12 +319,23 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain *chains
  * The whole decrypted body after the explicit IV (payload | MAC | padding, ct_len - IV
  * bytes) is written at pt + pt_off: size the plaintext slots for it.
  * CBC suites (AES, 3DES) decrypt every block of every record in parallel and need a
- * workspace of tlsgpu_open_workspace_bytes(nrecords) bytes (NULL = library-owned). */
+ * workspace of tlsgpu_open_workspace_bytes(nrecords) bytes (NULL = library-owned).
+ * wire: ciphertext arena of wire_bytes, pt: plaintext arena of pt_bytes, states: nstates
+ * states (ABI 6 bounds: a refused record gets status TLSGPU_EINVAL and is treated as if it
+ * were not in the batch).
+ * Large batches of short chains open in parts on a library-owned second stream beside the
+ * caller's.  Limits of that stream: one per (device, priority), so
+ * split opens issued at once on different caller streams of one priority run their decrypt
+ * passes one after another; and a caller stream under HIP graph capture pulls it into the
+ * capture.  tlsgpu_release_workspaces destroys it. */
 size_t tlsgpu_open_workspace_bytes(uint32_t nrecords);
 int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_open_record *records,
-                    uint32_t nrecords, const uint8_t *wire, uint8_t *pt, tlsgpu_conn_state *states,
-                    int32_t *status, uint32_t variant, void *workspace, size_t workspace_bytes,
-                    tlsgpu_stream s);
+                    uint32_t nrecords, const uint8_t *wire, size_t wire_bytes, uint8_t *pt, size_t pt_bytes,
+                    tlsgpu_conn_state *states, uint32_t nstates, int32_t *status, uint32_t variant,
+                    void *workspace, size_t workspace_bytes, tlsgpu_stream s);
+/* ABI 6: the record count from which an open runs in parts (n < 0: the library's default,
+ * 4 parts x 512 records per CU); tests lower it to exercise the parts path.  Process-wide. */
+int tlsgpu_set_open_parts_min_records(int64_t n);
 /* raw stateful encrypt (decrypt=0) / decrypt (decrypt=1) of spans; one span
  * per state per launch (a state's spans in one launch run in array order). */
 int tlsgpu_cipher_dev(const tlsgpu_span *spans, uint32_t nspans, const uint8_t *in, uint8_t *out,

@@ -30,6 +30,20 @@ def test_header_symbols_exported():
     assert set(decls) == bound, set(decls) ^ bound
 
 
+def test_binding_arity_matches_header():
+    """Every ctypes signature has as many arguments as the header's prototype (a missing
+    size argument would shift every later one: ABI 6 added the arena sizes)."""
+    from tlslite_amd import _native as N
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "tlsgpu.h")).read(), flags=re.S)
+    protos = {}
+    for m in re.finditer(r"\b(tlsgpu_\w+)\s*\(([^;{]*?)\)\s*;", src):
+        args = m.group(2).strip()
+        protos[m.group(1)] = 0 if args in ("", "void") else len(args.split(","))
+    for name, _, argtypes in N.SIGNATURES:
+        assert name in protos, name
+        assert len(argtypes) == protos[name], (name, len(argtypes), protos[name])
+
+
 def test_abi_structs_and_constants():
     from tlslite_amd import _native as N
     src = open(os.path.join(ROOT, "include", "tlsgpu.h")).read()
@@ -37,10 +51,10 @@ def test_abi_structs_and_constants():
                       ("TLSGPU_CIPHER_3DES", 4), ("TLSGPU_MAC_SHA1", 1), ("TLSGPU_MAC_SHA256", 2),
                       ("TLSGPU_MAC_MD5", 3), ("TLSGPU_ALERT_BAD_RECORD_MAC", -20),
                       ("TLSGPU_ALERT_DECRYPTION_FAILED", -21), ("TLSGPU_ALERT_SKIPPED", -22),
-                      ("TLSGPU_CONN_STATE_BYTES", 2048), ("TLSGPU_ABI_VERSION", 5)]:
+                      ("TLSGPU_CONN_STATE_BYTES", 2048), ("TLSGPU_ABI_VERSION", 6)]:
         assert re.search(r"\b%s\s*=?\s*%d\b" % (name, val), src), name
     assert re.search(r"#define TLSGPU_CHAIN_STOP_ON_ALERT 1u", src)
-    assert N.lib.tlsgpu_abi_version() == N.ABI_VERSION == 5
+    assert N.lib.tlsgpu_abi_version() == N.ABI_VERSION == 6
     assert (N.ALERT_SKIPPED, N.CHAIN_STOP_ON_ALERT) == (-22, 1)
     assert ctypes.sizeof(N.Record) == 24 and ctypes.sizeof(N.Chain) == 16
     assert [f[0] for f in N.Chain._fields_] == ["state", "first", "count", "flags"]

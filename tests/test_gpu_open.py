@@ -275,14 +275,14 @@ def test_stop_on_alert_like_connection(suite, version):
 def test_split_open_parts_like_oracle(suite, version):
     """The open in parts (launch_open_split: decrypt and padding pass of chain range h+1 on
     a second stream beside the MAC pass of range h; the library does this from 512 records
-    per CU per part, TLSGPU_OPEN_PARTS_MIN_RECORDS lowers the threshold here):
+    per CU per part, tlsgpu_set_open_parts_min_records lowers the threshold here):
     6,000 connections of 1-6 records of 1-700 B, ~3 % of records tampered or
     truncated, connection (stop-on-alert) semantics -- every status, plaintext and final
     state equals the oracle's, across the part boundaries (tlsrecordlayer.py:958-1044)."""
     from oracle import oracle as O
     from tlslite_amd import _native as N
     from tlslite_amd.device import cu_count
-    from tlslite_amd.recordlayer import open_records
+    from tlslite_amd.recordlayer import open_records, set_open_parts_min_records
     T = _T()
     rng = np.random.default_rng(zlib.crc32(repr(("parts", suite, version)).encode()))
     amap = {0: 0, O.ALERT_BAD_RECORD_MAC: N.ALERT_BAD_RECORD_MAC,
@@ -307,11 +307,11 @@ def test_split_open_parts_like_oracle(suite, version):
         elif u < 0.03:
             body = body[:-1]
         recs.append((ci, ct, bytes(body)))
-    os.environ["TLSGPU_OPEN_PARTS_MIN_RECORDS"] = "1"
+    set_open_parts_min_records(1)
     try:
         res = open_records(readers, recs)
     finally:
-        del os.environ["TLSGPU_OPEN_PARTS_MIN_RECORDS"]
+        set_open_parts_min_records(None)
     stopped = set()
     for (ci, ct, body), (st, p) in zip(recs, res):
         if ci in stopped:

@@ -5,6 +5,7 @@ sharding/aggregation test), and the gathered result must equal the
 single-process run; the max/sum reductions used for the bench line are
 exercised too."""
 import hashlib
+import json
 import os
 import socket
 
@@ -53,7 +54,7 @@ def _worker(rank, world, port, q):
     mine = shard_indices(6, rank, world)
     digests = _seal_shard(wl)
     by_global = {int(mine[c]): d for c, d in digests.items()}
-    allmaps = g.gather_bytes(repr(sorted(by_global.items())).encode())
+    allmaps = g.gather_bytes(json.dumps(sorted(by_global.items())).encode())
     t_max = g.max(1.0 + rank)
     total = g.sum(wl.plaintext_total)
     g.barrier()
@@ -77,7 +78,7 @@ def test_two_rank_sharding_matches_single_process():
     for rank, allmaps, t_max, total in res:
         merged = {}
         for m in allmaps:
-            merged.update(dict(eval(m.decode())))
+            merged.update({int(c): d for c, d in json.loads(m.decode())})
         assert merged == single
         assert t_max == 2.0
         assert total == 6 * 3 * 700
@@ -269,3 +270,19 @@ def test_shard_rendezvous_drops_foreign_peers():
         assert p.exitcode == 0
     s.close()
     assert res == [3.0, 3.0]
+
+
+def test_job_token_sources():
+    """The rendezvous token: the spawner's random token wins; torchrun's
+    TORCHELASTIC_RUN_ID when it is a real id; for torchrun's default "none" on one node, a
+    token from the master address/port and the launcher's PID (every local rank's parent)."""
+    from tlslite_amd.shard import job_token
+    assert job_token({"TLSGPU_RDZV_TOKEN": "abc", "TORCHELASTIC_RUN_ID": "x"}) == "abc"
+    assert job_token({"TORCHELASTIC_RUN_ID": "run-7"}) == "run-7"
+    env = {"TORCHELASTIC_RUN_ID": "none", "LOCAL_WORLD_SIZE": "2", "WORLD_SIZE": "2",
+           "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29533"}
+    assert job_token(env, ppid=4242) == "127.0.0.1:29533:4242"
+    assert job_token(env, ppid=4242) != job_token(env, ppid=4243)
+    # several nodes: the launchers' PIDs differ, so the PID cannot be part of the token
+    assert job_token(dict(env, WORLD_SIZE="4"), ppid=4242) == "none"
+    assert job_token({}) == ""

@@ -17,7 +17,7 @@ FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
 OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH = 0, -1, -2, -3, -4, -5
 ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED, ALERT_SKIPPED = -20, -21, -22
 CHAIN_STOP_ON_ALERT = 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 CONN_STATE_BYTES = 2048
 
 
@@ -97,17 +97,19 @@ SIGNATURES = [
     ("tlsgpu_seal_workspace_bytes", _sz, [_u32]),
     ("tlsgpu_release_workspaces", _i, []),
     ("tlsgpu_owned_workspace_count", _sz, []),
+    ("tlsgpu_owned_stream_count", _sz, []),
     ("tlsgpu_seal_cipher_kernel", _i, [_u32, _u32, ctypes.c_char_p, _sz]),
-    ("tlsgpu_seal_dev", _i, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
+    ("tlsgpu_seal_dev", _i, [_vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32, _vp, _sz, _vp]),
     ("tlsgpu_pipeline_create", _i, [ctypes.POINTER(_vp), _u32]),
     ("tlsgpu_pipeline_destroy", _i, [_vp]),
     ("tlsgpu_pipeline_synchronize", _i, [_vp]),
-    ("tlsgpu_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp]),
+    ("tlsgpu_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32, _vp, _vp]),
     ("tlsgpu_host_pipeline_create", _i, [ctypes.POINTER(_vp), _sz, _i]),
     ("tlsgpu_host_pipeline_destroy", _i, [_vp]),
-    ("tlsgpu_host_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _vp, _u32]),
+    ("tlsgpu_host_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32]),
     ("tlsgpu_open_workspace_bytes", _sz, [_u32]),
-    ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _sz, _vp]),
+    ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32, _vp, _sz, _vp]),
+    ("tlsgpu_set_open_parts_min_records", _i, [ctypes.c_int64]),
     ("tlsgpu_cipher_dev", _i, [_vp, _u32, _vp, _vp, _vp, _i, _i, _vp]),
     ("tlsgpu_derive_states_dev", _i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("tlsgpu_fill_pattern", _i, [_vp, _sz, _u64, _u64, _vp]),

@@ -16,7 +16,7 @@ LIB = os.path.join(LIBDIR, "libtlsgpu.so")
 ARCH = os.environ.get("TLSGPU_ARCH", "gfx950")
 
 SOURCES = ["tg_kernels.hip", "tg_api.hip"]
-HEADERS = ["tg_fused.h", "tg_common.h", "tg_hash.h", "tg_device.h", "tg_quad.h", "tg_aes3.h", "tg_open3.h", "tg_launch.h", "tg_keysched.h", "tg_derive.h"]
+HEADERS = ["tg_config.h", "tg_common.h", "tg_hash.h", "tg_device.h", "tg_quad.h", "tg_aes3.h", "tg_open3.h", "tg_launch.h", "tg_keysched.h", "tg_derive.h"]
 
 
 def _hipcc():
@@ -33,20 +33,24 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False, extra_flags=(), libdir=LIBDIR):
-    """Compile libtlsgpu.so into libdir.  extra_flags / libdir: A/B builds of the same
-    sources with a compile-time experiment switch (tools/build_ab.sh); the product is
-    the default build in tlslite_amd/lib."""
+def build(force=False, verbose=False, extra_flags=(), libdir=LIBDIR, overlay=None):
+    """Compile libtlsgpu.so into libdir.  extra_flags / libdir / overlay: experiment builds
+    of the same sources (tools/build_ab.sh): `overlay` is a directory searched before csrc
+    for <tg_config.h>, so its tuning constants (with -D overrides) replace the product's.
+    The product is the default build in tlslite_amd/lib, from csrc/tg_config.h."""
     lib = os.path.join(libdir, "libtlsgpu.so")
     os.makedirs(libdir, exist_ok=True)
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(HERE, "..", "include", "tlsgpu.h")]
-    if not force and not _stale(lib, deps):
-        return lib
     objs = []
     hipcc = _hipcc()
+    incs = (["-I" + overlay] if overlay else []) + ["-I" + CSRC]
+    if overlay:
+        deps += [os.path.join(overlay, f) for f in os.listdir(overlay)]
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
-             "-munsafe-fp-atomics"] + list(extra_flags)
+             "-munsafe-fp-atomics"] + incs + list(extra_flags)
+    if not force and not _stale(lib, deps):
+        return lib
     for s in srcs:
         o = os.path.join(libdir, os.path.basename(s) + ".o")
         cmd = [hipcc] + flags + ["-c", s, "-o", o]
@@ -62,10 +66,15 @@ def build(force=False, verbose=False, extra_flags=(), libdir=LIBDIR):
 
 
 if __name__ == "__main__":
-    # python tlslite_amd/build.py [--force] [--out DIR] [-DFLAG ...]
+    # python tlslite_amd/build.py [--force] [--out DIR --overlay DIR] [-DFLAG ...]
     args = sys.argv[1:]
     out = LIBDIR
+    overlay = None
     if "--out" in args:
         out = os.path.abspath(args[args.index("--out") + 1])
+    if "--overlay" in args:
+        overlay = os.path.abspath(args[args.index("--overlay") + 1])
+    if (overlay or any(a.startswith("-D") for a in args)) and out == LIBDIR:
+        sys.exit("build.py: experiment builds (--overlay / -D) go to --out DIR, never to the product lib/")
     flags = [a for a in args if a.startswith("-D")]
-    print(build(force="--force" in args or bool(flags), verbose=True, extra_flags=flags, libdir=out))
+    print(build(force="--force" in args or bool(flags), verbose=True, extra_flags=flags, libdir=out, overlay=overlay))

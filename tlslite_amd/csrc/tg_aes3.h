@@ -22,6 +22,7 @@
 // batch k the cipher waves win issue arbitration.
 #pragma once
 #include "tg_quad.h"
+#include <tg_config.h>
 
 namespace tg {
 
@@ -35,50 +36,42 @@ struct RecMeta {
 };
 static_assert(sizeof(RecMeta) == 32, "RecMeta");
 constexpr uint32_t TAIL_SLOT = 64;
-#ifndef TG_AB_CBC_WAVES
-#define TG_AB_CBC_WAVES 16
-#endif
-constexpr int C3_THREADS = 64 * TG_AB_CBC_WAVES;  // 16 cipher waves
-constexpr int C3_CHAINS = 16 * TG_AB_CBC_WAVES;
+constexpr int C3_THREADS = 64 * CFG_CBC_WAVES;  // 16 cipher waves
+constexpr int C3_CHAINS = 16 * CFG_CBC_WAVES;
 // Many-chains regime (more chains than one generation of 16-wave workgroups, cfg3): the MAC
 // kernel at <= 128 VGPRs with a one-chunk prefetch.  Beside the pair cipher kernel (8 waves
 // per CU, 89 VGPRs: 2 x 96 allocated per SIMD) two MAC waves per SIMD fit with either MAC
 // form; the two-chunk ring at launch bound 3 (148 VGPRs) measured 1.5 % slower on cfg3 in
-// round 4 (profiles/r04/ab/ab_cfg3_r04.txt).  C3_WAVES_MANY: the quad cipher kernel's waves
-// in this regime (TG_AB_NO_PAIR builds only; 12, so that two MAC waves fit beside them:
-// 3 x 80 + 2 x 128 <= 512)
-#ifndef TG_AB_WAVES_MANY
-#define TG_AB_WAVES_MANY 12
-#endif
-constexpr int C3_WAVES_MANY = TG_AB_WAVES_MANY;
-#ifndef TG_AB_MAC_LB_MANY
-#define TG_AB_MAC_LB_MANY 4
-#endif
-#ifndef TG_AB_MAC_PF_MANY
-#define TG_AB_MAC_PF_MANY 1
-#endif
-constexpr int MAC_LB_MANY = TG_AB_MAC_LB_MANY, MAC_PF_MANY = TG_AB_MAC_PF_MANY;
+// round 4 (profiles/r04/ab/ab_cfg3_r04.txt).
+constexpr int MAC_LB_MANY = CFG_MAC_LB_MANY, MAC_PF_MANY = CFG_MAC_PF_MANY;
 
 template <int CIPHER_ID, int MAC, bool SSL3>
 __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains,
                                                     const tlsgpu_record* __restrict__ recs,
                                                     ConnState* __restrict__ states, int32_t* __restrict__ wire_len,
                                                     RecMeta* __restrict__ meta, uint32_t nrecords, uint32_t epoch,
-                                                    uint64_t wire_cap) {
+                                                    uint64_t pt_cap, uint64_t wire_cap, uint32_t nstates) {
     const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
-    ConnState* st = states + ch.state;
+    // a state index outside the caller's array: every record of the chain is refused and no
+    // state is read (ABI 6)
+    const bool sok = ch.state < nstates;
+    ConnState* st = states + (sok ? ch.state : 0u);
     // the state's first 32 bytes in two 16-byte loads (one line request), tested without
     // short-circuit branches: field-by-field loads behind each comparison cost a dependent
     // memory latency apiece (cfg3: 1 Mi chains)
-    const uint4 h0 = *(const uint4*)st;                          // cipher, mac, vmaj..maclen, ssl3
-    const uint4 h1 = *(const uint4*)((const uint8_t*)st + 16);   // seqnum (lo, hi), explicit_iv, raw
+    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = make_uint4(0, 0, 0, 0);
+    if (sok) {
+        h0 = *(const uint4*)st;                          // cipher, mac, vmaj..maclen, ssl3
+        h1 = *(const uint4*)((const uint8_t*)st + 16);   // seqnum (lo, hi), explicit_iv, raw
+    }
     static_assert(__builtin_offsetof(ConnState, mac) == 4 && __builtin_offsetof(ConnState, ssl3) == 12 &&
                       __builtin_offsetof(ConnState, seqnum) == 16 && __builtin_offsetof(ConnState, explicit_iv) == 24 &&
                       __builtin_offsetof(ConnState, raw) == 28,
                   "state header layout");
-    const bool ok = (h0.x == (uint32_t)CIPHER_ID) & (h0.y == (uint32_t)MAC) & (h0.w == (SSL3 ? 1u : 0u)) & (h1.w == 0u);
+    const bool ok = sok & (h0.x == (uint32_t)CIPHER_ID) & (h0.y == (uint32_t)MAC) & (h0.w == (SSL3 ? 1u : 0u)) &
+                    (h1.w == 0u);
     constexpr int DL = Hash<MAC>::DLEN;
     constexpr uint32_t BS = CIPHER_ID == TLSGPU_CIPHER_3DES ? 8u : 16u;
     uint64_t seq = (uint64_t)h1.x | ((uint64_t)h1.y << 32);
@@ -94,17 +87,18 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
         m.tail_len = 0;
         m.pad[0] = m.pad[1] = 0;
         if (!ok) {
-            wire_len[r] = TLSGPU_EMISMATCH;
+            wire_len[r] = sok ? TLSGPU_EMISMATCH : TLSGPU_EINVAL;
         } else {
-            const uint32_t n = recs[r].pt_len;
+            const tlsgpu_record R = recs[r];
+            const uint32_t n = R.pt_len;
             const uint32_t cur = E + n + DL;
             const uint32_t body = cur + (BS - (cur & (BS - 1)));
             if (n == 0) {
                 wire_len[r] = 0;
             } else if (body > 0xffffu) {
                 wire_len[r] = TLSGPU_ETOOBIG;
-            } else if ((uint64_t)recs[r].wire_off + 5u + body > wire_cap) {
-                wire_len[r] = TLSGPU_EINVAL;  // the sealed record would end past the wire arena
+            } else if (!in_arena(R.pt_off, n, pt_cap) || !in_arena(R.wire_off, 5u + body, wire_cap)) {
+                wire_len[r] = TLSGPU_EINVAL;  // the record would read / write outside the caller's arenas
             } else {
                 const uint32_t rb = n & (BS - 1);
                 m.status = 1;
@@ -117,37 +111,11 @@ __global__ void __launch_bounds__(256) prefix_kernel(const tlsgpu_chain* __restr
     if (ok) st->seqnum = seq;
 }
 
-// Compile-time experiment switches (tools/build_ab.sh builds them into separate
-// libraries; the product build defines none).  Each selects another correct configuration
-// of the product kernels.  Variants measured slower and not kept (non-temporal loads /
-// stores, v_perm byte-1 addresses, v_cndmask transposes, flat loads, v_and_or 3DES
-// addresses) were removed in round 3, and the timing-only probes of the MAC phase (no MAC,
-// MAC without loads / compressions / transposes: wrong output by design) in round 4 (last
-// in commit 4f1633b); their results are in DESIGN.md and profiles/r0{2,3}/.
-//   TG_AB_MAC_PRIO / TG_AB_CBC_PRIO  wave priorities of the MAC / cipher waves
-//   TG_AB_MAC_PF        chunks the cooperative MAC loop prefetches (default 2)
-//   TG_AB_MAC_LB        mac_kernel's launch bound in 256-thread blocks per CU (default 3)
-//   TG_AB_CBC_WAVES     cipher waves per CU (default 16: 256 chains)
-//   TG_AB_NO_MANY       no many-chains configuration (12 cipher waves + 128-VGPR MAC kernel, cfg3)
-//   TG_AB_WAVES_MANY    cipher waves per CU in the many-chains configuration (default 12)
-//   TG_AB_MAC_LB_MANY / TG_AB_MAC_PF_MANY  launch bound / prefetch ring of the many-chains MAC kernel
-//   TG_AB_NO_PAIR    cipher phase on the quad layout (cbc_kernel) in the throughput regimes too,
-//                    instead of 2 lanes per chain (cbc_pair_kernel)
-//   TG_AB_FUSED      the one-kernel seal (seal_fused_kernel, tg_fused.h) in the pair regime instead
-//                    of the split prefix / MAC / cbc_pair_kernel path; TG_AB_FUSED_G / _GM: its
-//                    prefetch group in the one-generation / many-chains regime; TG_AB_FZ_*: its
-//                    MAC waves' priority, gating and lead (tg_fused.h)
-//   TG_AB_OPEN_NOSPLIT  the open path's passes once on the caller's stream (no parts beside
-//                    a second stream, launch_open_split)
-//   TG_AB_PAIR_G1 / TG_AB_PAIR_GM  the pair kernel's prefetch group (blocks) in the one-generation
-//                    (cfg2) / many-chains (cfg3) regime; TG_AB_PAIR_MAC_MANY: the 128-VGPR MAC
-//                    kernel in the one-generation pair regime too
-#ifndef TG_AB_MAC_PRIO
-#define TG_AB_MAC_PRIO 0
-#endif
-#ifndef TG_AB_CBC_PRIO
-#define TG_AB_CBC_PRIO 1
-#endif
+// Tuning constants: tg_config.h (experiment builds replace it, tools/build_ab.sh).  Variants
+// measured slower and not kept -- non-temporal loads / stores, v_perm byte-1 addresses,
+// v_cndmask transposes, flat loads, the quad cipher layout in the throughput regimes, 12
+// cipher waves with a 128-VGPR MAC kernel, the one-kernel seal (last in
+// commit c22dfb8, tlslite_amd/csrc/tg_fused.h) -- are in DESIGN.md and profiles/r0{2,3,4}/.
 
 // 64-byte chunk load: 4 x dwordx4 when 16-byte aligned, else the generic path
 template <bool AL16>
@@ -180,10 +148,7 @@ __device__ __forceinline__ void mac_bulk(M& mac, const uint8_t* P, uint32_t nful
     }
 }
 
-#ifndef TG_AB_MAC_PF
-#define TG_AB_MAC_PF 2
-#endif
-constexpr int MAC_PF = TG_AB_MAC_PF;  // chunks prefetched ahead by the cooperative MAC loop
+constexpr int MAC_PF = CFG_MAC_PF;  // chunks prefetched ahead by the cooperative MAC loop
 
 // 16-byte load through a global-address-space pointer: the quad's record pointers are
 // rebuilt from DPP-exchanged integers, which the compiler would otherwise turn into
@@ -310,11 +275,8 @@ __device__ __forceinline__ void mac_bulk_coop(M& mac, const uint8_t* P, uint32_t
 
 // Register budget: a MAC wave must fit beside four cbc_kernel waves on a SIMD
 // (4 x 80 + 168 <= 512 VGPRs) for the pipeline to overlap the two phases: the launch
-// bound's 3 waves per SIMD caps it at 168.  (TG_AB_MAC_LB: the A/B of that bound.)
-#ifndef TG_AB_MAC_LB
-#define TG_AB_MAC_LB 3
-#endif
-template <int MAC, bool SSL3, int BS = 16, int LB = TG_AB_MAC_LB, int PF = MAC_PF>
+// bound's 3 waves per SIMD caps it at 168.
+template <int MAC, bool SSL3, int BS = 16, int LB = CFG_MAC_LB, int PF = MAC_PF>
 __global__ void __launch_bounds__(256, LB) mac_kernel(const tlsgpu_record* __restrict__ recs, uint32_t nrecords,
                                                  const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
                                                  const ConnState* __restrict__ states, int32_t* __restrict__ wire_len,
@@ -330,7 +292,7 @@ __global__ void __launch_bounds__(256, LB) mac_kernel(const tlsgpu_record* __res
         mt = meta[r];
         act = mt.epoch == epoch && mt.status == 1;
     }
-    __builtin_amdgcn_s_setprio(TG_AB_MAC_PRIO);
+    __builtin_amdgcn_s_setprio(CFG_MAC_PRIO);
     const ConnState* st = states;
     tlsgpu_record R = {};
     const uint8_t* P = pt;
@@ -489,12 +451,12 @@ __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t*
 
 // LAT: the few-chains (latency) form of the round, QuadAes::round; the launcher picks it
 // when a CU gets fewer chains than it has quads (cfg4), the throughput form otherwise
-template <int NR, bool LAT, int WAVES = TG_AB_CBC_WAVES>
+template <int NR, bool LAT, int WAVES = CFG_CBC_WAVES>
 __global__ void __launch_bounds__(64 * WAVES, 1)
 cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
            uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
            ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,
-           uint32_t cpw, uint32_t epoch) {
+           uint32_t cpw, uint32_t epoch, uint32_t nstates) {
     aes_lds_fill(nullptr, false);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
@@ -513,7 +475,7 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
     if (local >= cpw && (threadIdx.x >> 6) == 0 && (uint64_t)gridDim.x * cpw >= nchains) local %= cpw;
     if (local >= cpw) return;
     // the prefix kernel validated the state: any record it marked status 1 belongs to a matching state
-    __builtin_amdgcn_s_setprio(TG_AB_CBC_PRIO);
+    __builtin_amdgcn_s_setprio(CFG_CBC_PRIO);
     QuadAes aes;
     aes.init();
     // persistent over chain generations: with more chains than CUs x cpw (cfg3: 4,096 chains per
@@ -521,6 +483,7 @@ cbc_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsg
     // workgroup drain / relaunch between generations (cfg3 cipher phase 2.96 -> 2.26 ms)
     for (uint32_t cid = blockIdx.x * cpw + local; cid < nchains; cid += gridDim.x * cpw) {
     const tlsgpu_chain ch = chains[cid];
+    if (ch.state >= nstates) continue;  // refused by the prefix kernel (ABI 6): no state read
     ConnState* st = states + ch.state;
     uint32_t k[NR + 1];
     uint32_t iv = st->iv[q];
@@ -603,28 +566,12 @@ __device__ __forceinline__ void pair_block(const PairAes& aes, const uint32_t* k
 //   many chains (cfg3): 8 waves, 4-block groups (95 VGPRs for AES-256) + two 128-VGPR MAC
 //   waves per SIMD (the MAC phase is that regime's critical path): cfg3 523 -> 540 GiB/s.
 constexpr int PAIR_WAVES = 8;
-#ifndef TG_AB_PAIR_WM
-#define TG_AB_PAIR_WM 8  // waves per CU in the many-chains regime
-#endif
-constexpr int PAIR_WAVES_MANY = TG_AB_PAIR_WM;
-#ifndef TG_AB_PAIR_G1
-#define TG_AB_PAIR_G1 8
-#endif
-#ifndef TG_AB_PAIR_GM
-#define TG_AB_PAIR_GM 4
-#endif
+constexpr int PAIR_WAVES_MANY = CFG_PAIR_WAVES_MANY;  // waves per CU in the many-chains regime
 
-// Progress hook of the cipher's plaintext loads: the fused seal kernel (tg_fused.h) tells its
-// MAC waves how far a chain's loads have been issued (NoPub: the split path, nothing to tell).
-struct NoPub {
-    __device__ __forceinline__ void operator()(uint32_t /*blocks issued in the bulk*/) const {}
-};
-
-template <int NR, int G, bool AL, bool CLAMP, class Pub = NoPub>
+template <int NR, int G, bool AL, bool CLAMP>
 __device__ __forceinline__ void pcbc_group(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
                                            const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
-                                           uint8_t* O, uint32_t b0, uint32_t last, uint2 f[G],
-                                           const Pub& pub = Pub()) {
+                                           uint8_t* O, uint32_t b0, uint32_t last, uint2 f[G]) {
     constexpr int PAIR_G = G;
     uint2 c[PAIR_G];
 #pragma unroll
@@ -640,7 +587,6 @@ __device__ __forceinline__ void pcbc_group(const PairAes& aes, const uint32_t* k
 #pragma unroll
         for (int i = 0; i < PAIR_G; i++) f[i] = ld64t<AL>(Pn + 16 * i);
     }
-    pub(CLAMP ? last + 1 : b0 + 2 * PAIR_G);  // blocks of P (this bulk) whose loads are issued
     uint8_t* Ob = O + 16 * b0;
     // the group's ciphertext is kept in registers and stored at the group's end: the chain's
     // stores reach the L2 together and merge into whole lines (with aligned groups, pcbc_bulk)
@@ -656,19 +602,10 @@ __device__ __forceinline__ void pcbc_group(const PairAes& aes, const uint32_t* k
 
 constexpr uint32_t PAIR_ALIGN_MIN = 16;  // blocks: records this long align their groups
 
-// Pub: called with the number of the record's blocks whose loads are issued (the hook is
-// handed the group loop's counts shifted by the head)
-template <class Pub>
-struct PubShift {
-    const Pub& pub;
-    uint32_t head;
-    __device__ __forceinline__ void operator()(uint32_t b) const { pub(head + b); }
-};
-
-template <int NR, int GI, bool AL, class Pub = NoPub>
+template <int NR, int GI, bool AL>
 __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
                                           const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
-                                          uint8_t* O, uint32_t nb, const Pub& pub = Pub()) {
+                                          uint8_t* O, uint32_t nb) {
     if (nb == 0) return;
     constexpr uint32_t G = GI;
     // Records of at least PAIR_ALIGN_MIN blocks first run the head blocks up to the output's
@@ -697,8 +634,6 @@ __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw
 #pragma unroll
         for (int i = 0; i < (int)G; i++) f[i] = ld64t<AL>(Pg + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
     }
-    pub(head + (ng < G ? ng : G));
-    const PubShift<Pub> gpub{pub, head};
 #pragma unroll
     for (int i = 0; i < (int)G; i++)
         if ((uint32_t)i < head) {
@@ -708,12 +643,12 @@ __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw
     if (ng == 0) return;
     uint32_t b0 = 0;
     if (ng >= 2 * G) {  // first group peeled, as cbc_bulk
-        pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, 0, last, f, gpub);
+        pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, 0, last, f);
         for (b0 = G; b0 + 2 * G <= ng; b0 += G)
-            pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f, gpub);
+            pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f);
     }
     if (b0 + G <= ng) {
-        pcbc_group<NR, GI, AL, true>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f, gpub);
+        pcbc_group<NR, GI, AL, true>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f);
         b0 += G;
     }
 #pragma unroll
@@ -730,19 +665,20 @@ __global__ void __launch_bounds__(64 * WAVES, 1)
 cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
                 uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
                 ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,
-                uint32_t cpw, uint32_t epoch) {
+                uint32_t cpw, uint32_t epoch, uint32_t nstates) {
     aes_lds_fill(nullptr, false);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t local = (threadIdx.x >> 6) * 32 + (lane >> 1);
     const uint32_t h = lane & 1;
     if (local >= cpw) return;  // both lanes of a pair leave together
-    __builtin_amdgcn_s_setprio(TG_AB_CBC_PRIO);
+    __builtin_amdgcn_s_setprio(CFG_CBC_PRIO);
     PairAes aes;
     aes.init();
     // persistent over chain generations (as cbc_kernel)
     for (uint32_t cid = blockIdx.x * cpw + local; cid < nchains; cid += gridDim.x * cpw) {
         const tlsgpu_chain ch = chains[cid];
+        if (ch.state >= nstates) continue;  // refused by the prefix kernel (ABI 6): no state read
         ConnState* st = states + ch.state;
         uint32_t kw[2], ka[NR + 1], kb[NR + 1];
         PairAes::round_keys<NR>(st->ek, h, kw, ka, kb);
@@ -902,7 +838,7 @@ __global__ void __launch_bounds__(D4_THREADS, 1)
 tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tlsgpu_record* __restrict__ recs,
              uint32_t nrecords, const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
              ConnState* __restrict__ states, const RecMeta* __restrict__ meta, const uint8_t* __restrict__ tails,
-             uint32_t cpw, uint32_t epoch) {
+             uint32_t cpw, uint32_t epoch, uint32_t nstates) {
     // combined tables at LDS offset 0 (the kernel's only LDS), read back by absolute address (Des4C::f)
     extern __shared__ __attribute__((aligned(16))) uint32_t d4_lds[];
     des_lds_fill_comb(d4_lds);
@@ -912,6 +848,7 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
     const uint32_t cid = blockIdx.x * cpw + local;
     if (local >= cpw || cid >= nchains) return;  // the 4 lanes of a chain leave together
     const tlsgpu_chain ch = chains[cid];
+    if (ch.state >= nstates) return;  // refused by the prefix kernel (ABI 6): no state read
     ConnState* st = states + ch.state;
     Des4C D;
     D.init();

@@ -15,6 +15,7 @@
 #include "tg_hash.h"
 #include "tg_keysched.h"
 #include "tg_launch.h"
+#include <tg_config.h>
 
 using namespace tg;
 
@@ -330,8 +331,13 @@ hipError_t own_release_stream(hipStream_t s) {
 extern "C" {
 
 int tlsgpu_release_workspaces(void) {
-    std::lock_guard<std::mutex> g(own_mu);
-    hipError_t e = own_release([](const OwnKey&) { return true; }, true);
+    hipError_t e;
+    {
+        std::lock_guard<std::mutex> g(own_mu);
+        e = own_release([](const OwnKey&) { return true; }, true);
+    }
+    const hipError_t e2 = release_open_aux();  // the split open's second streams and events
+    if (e == hipSuccess) e = e2;
     if (e != hipSuccess) return fail_hip(e, "tlsgpu_release_workspaces");
     return 0;
 }
@@ -339,6 +345,13 @@ int tlsgpu_release_workspaces(void) {
 size_t tlsgpu_owned_workspace_count(void) {
     std::lock_guard<std::mutex> g(own_mu);
     return own_bufs.size();
+}
+
+size_t tlsgpu_owned_stream_count(void) { return open_aux_count(); }
+
+int tlsgpu_set_open_parts_min_records(int64_t n) {
+    set_open_parts_min_records(n);
+    return 0;
 }
 
 static int own_workspace(int kind, size_t need, hipStream_t stream, uint8_t** out) {
@@ -367,8 +380,9 @@ static uint32_t next_epoch() {
 }
 
 int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* records, uint32_t nrecords,
-                    const uint8_t* pt, uint8_t* wire, tlsgpu_conn_state* states, int32_t* wire_len, uint32_t variant,
-                    void* workspace, size_t workspace_bytes, tlsgpu_stream s) {
+                    const uint8_t* pt, size_t pt_bytes, uint8_t* wire, size_t wire_bytes, tlsgpu_conn_state* states,
+                    uint32_t nstates, int32_t* wire_len, uint32_t variant, void* workspace, size_t workspace_bytes,
+                    tlsgpu_stream s) {
     if (nchains == 0) return 0;
     if (!chains || !records || !pt || !wire || !states || !wire_len) return fail(TLSGPU_EINVAL, "null pointer");
     uint8_t* ws = static_cast<uint8_t*>(workspace);
@@ -380,9 +394,13 @@ int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_r
             if (rc) return rc;
         }
     }
+    Bounds b;
+    b.pt_cap = pt_bytes;
+    b.wire_cap = wire_bytes;
+    b.nstates = nstates;
     bool known = false;
     hipError_t e = launch_seal(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len, ws,
-                               next_epoch(), HS(s), &known);
+                               next_epoch(), HS(s), &known, b);
     if (!known) return fail(TLSGPU_EINVAL, "unsupported seal variant");
     if (e != hipSuccess) return fail_hip(e, "seal launch");
     return 0;
@@ -391,10 +409,7 @@ int tlsgpu_seal_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_r
 // ---------------------------------------------------------------- pipeline
 // Workspaces in rotation: the MAC phase of call k reuses the workspace of call k - PIPE_WS,
 // so the MAC stream may run up to PIPE_WS - 1 calls ahead of the cipher stream.
-#ifndef TG_AB_PIPE_WS
-#define TG_AB_PIPE_WS 3
-#endif
-constexpr int PIPE_WS = TG_AB_PIPE_WS;
+constexpr int PIPE_WS = CFG_PIPE_WS;
 struct tlsgpu_pipeline_s {
     int dev;
     hipStream_t mac_s, cbc_s;
@@ -454,9 +469,9 @@ int tlsgpu_pipeline_synchronize(tlsgpu_pipeline p) {
 }
 
 int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain* chains, uint32_t nchains,
-                         const tlsgpu_record* records, uint32_t nrecords, const uint8_t* pt, uint8_t* wire,
-                         tlsgpu_conn_state* states, int32_t* wire_len, uint32_t variant, tlsgpu_event cipher_start,
-                         tlsgpu_event cipher_stop) {
+                         const tlsgpu_record* records, uint32_t nrecords, const uint8_t* pt, size_t pt_bytes,
+                         uint8_t* wire, size_t wire_bytes, tlsgpu_conn_state* states, uint32_t nstates,
+                         int32_t* wire_len, uint32_t variant, tlsgpu_event cipher_start, tlsgpu_event cipher_stop) {
     if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
     if (nchains == 0) return 0;
     if (!chains || !records || !pt || !wire || !states || !wire_len) return fail(TLSGPU_EINVAL, "null pointer");
@@ -464,6 +479,10 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain* chains, uint32_t
     static uint32_t epoch_ctr = 0x80000000u;
     const uint32_t epoch = __atomic_add_fetch(&epoch_ctr, 1, __ATOMIC_RELAXED);
     const int i = (int)(p->k % PIPE_WS);
+    Bounds b;
+    b.pt_cap = pt_bytes;
+    b.wire_cap = wire_bytes;
+    b.nstates = nstates;
     // workspace i was last read by the cipher phase of call k - PIPE_WS
     if (p->k >= (uint64_t)PIPE_WS) TG_HIP(hipStreamWaitEvent(p->mac_s, p->cbc_done[i], 0));
     bool known = false;
@@ -472,12 +491,12 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain* chains, uint32_t
         e = launch_seal_phases(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len,
                                static_cast<uint8_t*>(p->ws[i]), epoch, p->mac_s, p->mac_done[i], p->cbc_s,
                                reinterpret_cast<hipEvent_t>(cipher_start), reinterpret_cast<hipEvent_t>(cipher_stop),
-                               &known);
+                               &known, b);
     } else {
         // single-kernel variants run on the cipher stream, in order with earlier calls
         if (cipher_start) TG_HIP(hipEventRecord(reinterpret_cast<hipEvent_t>(cipher_start), p->cbc_s));
         e = launch_seal(variant, chains, nchains, records, nrecords, pt, wire, S(states), wire_len, nullptr, epoch,
-                        p->cbc_s, &known);
+                        p->cbc_s, &known, b);
         if (e == hipSuccess && cipher_stop) e = hipEventRecord(reinterpret_cast<hipEvent_t>(cipher_stop), p->cbc_s);
     }
     if (!known) return fail(TLSGPU_EINVAL, "unsupported seal variant");
@@ -674,7 +693,7 @@ static uint64_t sealed_max_bytes(uint32_t variant, uint64_t n) {
 int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains, uint32_t nchains,
                               const tlsgpu_record* records, uint32_t nrecords, const uint8_t* pt_host,
                               size_t pt_bytes, uint8_t* wire_host, size_t wire_bytes, tlsgpu_conn_state* states,
-                              int32_t* wire_len_host, uint32_t variant) {
+                              uint32_t nstates, int32_t* wire_len_host, uint32_t variant) {
     if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
     if (nchains == 0) return 0;
     if (!chains || !records || !pt_host || !wire_host || !states || !wire_len_host)
@@ -690,6 +709,7 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
         for (uint32_t c = 0; c < nchains; c++) {
             const tlsgpu_chain& ch = chains[c];
             if ((uint64_t)ch.first + ch.count > nrecords) return fail(TLSGPU_EINVAL, "chain outside the records");
+            if (ch.state >= nstates) return fail(TLSGPU_EINVAL, "chain state outside the states array");
             if (ch.count) {
                 cur.r0 = ch.first < cur.r0 ? ch.first : cur.r0;
                 cur.r1 = ch.first + ch.count > cur.r1 ? ch.first + ch.count : cur.r1;
@@ -798,17 +818,23 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
         bool known = false;
         hipError_t e;
         if (need_ws) {
-            SealBounds sb;
+            Bounds sb;
             sb.rec_lo = b.r0 < b.r1 ? b.r0 : 0;
             sb.rec_hi = b.r0 < b.r1 ? b.r1 : 0;
+            sb.pt_cap = pt_bytes;
             sb.wire_cap = wire_bytes;
+            sb.nstates = nstates;
             e = launch_seal_phases(variant, d_chains + b.c0, b.c1 - b.c0, d_recs, nrecords, p->pt.u8(), p->wire.u8(),
                                    S(states), static_cast<int32_t*>(p->len.p), p->ws[t].u8(), next_epoch(), p->mac,
                                    p->mac_done[t], p->cbc, nullptr, nullptr, &known, sb);
         } else {  // single-kernel variants (RC4) on the cipher stream
             TG_HIP(hipStreamWaitEvent(p->cbc, p->in_done[t], 0));
+            Bounds rb;
+            rb.pt_cap = pt_bytes;
+            rb.wire_cap = wire_bytes;
+            rb.nstates = nstates;
             e = launch_seal(variant, d_chains + b.c0, b.c1 - b.c0, d_recs, nrecords, p->pt.u8(), p->wire.u8(),
-                            S(states), static_cast<int32_t*>(p->len.p), nullptr, next_epoch(), p->cbc, &known);
+                            S(states), static_cast<int32_t*>(p->len.p), nullptr, next_epoch(), p->cbc, &known, rb);
         }
         if (!known) return fail(TLSGPU_EINVAL, "unsupported seal variant");
         if (e != hipSuccess) return fail_hip(e, "host pipeline seal");
@@ -849,8 +875,9 @@ int tlsgpu_cipher_dev(const tlsgpu_span* spans, uint32_t nspans, const uint8_t* 
 size_t tlsgpu_open_workspace_bytes(uint32_t nrecords) { return open_workspace_bytes(nrecords); }
 
 int tlsgpu_open_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* records,
-                    uint32_t nrecords, const uint8_t* wire, uint8_t* pt, tlsgpu_conn_state* states, int32_t* status,
-                    uint32_t variant, void* workspace, size_t workspace_bytes, tlsgpu_stream s) {
+                    uint32_t nrecords, const uint8_t* wire, size_t wire_bytes, uint8_t* pt, size_t pt_bytes,
+                    tlsgpu_conn_state* states, uint32_t nstates, int32_t* status, uint32_t variant, void* workspace,
+                    size_t workspace_bytes, tlsgpu_stream s) {
     if (nchains == 0) return 0;
     if (!chains || !records || !wire || !pt || !states || !status) return fail(TLSGPU_EINVAL, "null pointer");
     uint8_t* ws = static_cast<uint8_t*>(workspace);
@@ -862,9 +889,13 @@ int tlsgpu_open_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_o
             if (rc) return rc;
         }
     }
+    Bounds b;
+    b.pt_cap = pt_bytes;
+    b.wire_cap = wire_bytes;
+    b.nstates = nstates;
     bool known = false;
     hipError_t e = launch_open(variant, chains, nchains, records, nrecords, wire, pt, S(states), status, ws,
-                               next_epoch(), HS(s), &known);
+                               next_epoch(), HS(s), &known, b);
     if (!known) return fail(TLSGPU_EINVAL, "unsupported open variant");
     if (e != hipSuccess) return fail_hip(e, "open launch");
     return 0;

@@ -11,6 +11,12 @@
 
 namespace tg {
 
+// [off, off + len) lies inside an arena of cap bytes (no wrap-around): the per-record range
+// check of the seal / open kernels against the caller's arena sizes (ABI 6)
+__host__ __device__ inline bool in_arena(uint64_t off, uint64_t len, uint64_t cap) {
+    return len <= cap && off <= cap - len;
+}
+
 // ---------------------------------------------------------------- state
 // Device-resident connection state (one per connection / chain).  All byte
 // strings that feed the cipher are packed as little-endian dwords in stream

@@ -18,9 +18,6 @@
 #include "tg_device.h"
 #include "tg_quad.h"
 #include "tg_aes3.h"
-#ifdef TG_AB_FUSED
-#include "tg_fused.h"
-#endif
 #include "tg_open3.h"
 #include "tg_derive.h"
 #include "tg_launch.h"
@@ -38,17 +35,23 @@ __global__ void __launch_bounds__(SEAL_BLOCK) rc4_seal_kernel(const tlsgpu_chain
                                                              const tlsgpu_record* __restrict__ recs,
                                                              const uint8_t* __restrict__ pt, uint8_t* __restrict__ wire,
                                                              ConnState* __restrict__ states,
-                                                             int32_t* __restrict__ wire_len) {
+                                                             int32_t* __restrict__ wire_len, uint32_t nrecords,
+                                                             uint64_t pt_cap, uint64_t wire_cap, uint32_t nstates) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
-    ConnState* st = states + ch.state;
+    const uint32_t cnt = ch.first >= nrecords ? 0u : min(ch.count, nrecords - ch.first);  // records past nrecords: ignored
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
+    if (ch.state >= nstates) {  // a state outside the caller's array: refused, nothing read (ABI 6)
+        for (uint32_t k = 0; k < cnt; k++) wire_len[ch.first + k] = TLSGPU_EINVAL;
+        return;
+    }
+    ConnState* st = states + ch.state;
     if (st->cipher != (uint32_t)TLSGPU_CIPHER_RC4 || st->mac != (uint32_t)MAC || st->ssl3 != (SSL3 ? 1u : 0u) ||
         st->raw) {
-        for (uint32_t k = 0; k < ch.count; k++) wire_len[ch.first + k] = TLSGPU_EMISMATCH;
+        for (uint32_t k = 0; k < cnt; k++) wire_len[ch.first + k] = TLSGPU_EMISMATCH;
         return;
     }
     Rc4Stream cipher;
@@ -56,7 +59,7 @@ __global__ void __launch_bounds__(SEAL_BLOCK) rc4_seal_kernel(const tlsgpu_chain
     uint64_t seq = st->seqnum;
     const uint32_t vmaj = st->vmaj, vmin = st->vmin;
 
-    for (uint32_t k = 0; k < ch.count; k++) {
+    for (uint32_t k = 0; k < cnt; k++) {
         const tlsgpu_record R = recs[ch.first + k];
         const uint32_t n = R.pt_len;
         if (n == 0) {  // empty record: nothing sent, no seqnum consumed (tlsrecordlayer.py:551-556)
@@ -66,6 +69,10 @@ __global__ void __launch_bounds__(SEAL_BLOCK) rc4_seal_kernel(const tlsgpu_chain
         const uint32_t body = n + DL;
         if (body > 0xffffu) {
             wire_len[ch.first + k] = TLSGPU_ETOOBIG;
+            continue;
+        }
+        if (!in_arena(R.pt_off, n, pt_cap) || !in_arena(R.wire_off, 5u + body, wire_cap)) {
+            wire_len[ch.first + k] = TLSGPU_EINVAL;  // outside the caller's arenas: nothing written, no seqnum
             continue;
         }
         const uint8_t* P = pt + R.pt_off;
@@ -212,28 +219,38 @@ __global__ void __launch_bounds__(SEAL_BLOCK) rc4_open_kernel(const tlsgpu_chain
                                                              const tlsgpu_open_record* __restrict__ recs,
                                                              const uint8_t* __restrict__ wire,
                                                              uint8_t* __restrict__ pt, ConnState* __restrict__ states,
-                                                             int32_t* __restrict__ status) {
+                                                             int32_t* __restrict__ status, uint32_t nrecords,
+                                                             uint64_t wire_cap, uint64_t pt_cap, uint32_t nstates) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
-    ConnState* st = states + ch.state;
+    const uint32_t cnt = ch.first >= nrecords ? 0u : min(ch.count, nrecords - ch.first);  // records past nrecords: ignored
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
+    if (ch.state >= nstates) {  // a state outside the caller's array: refused, nothing read (ABI 6)
+        for (uint32_t k = 0; k < cnt; k++) status[ch.first + k] = TLSGPU_EINVAL;
+        return;
+    }
+    ConnState* st = states + ch.state;
     if (st->cipher != (uint32_t)TLSGPU_CIPHER_RC4 || st->mac != (uint32_t)MAC || st->ssl3 != (SSL3 ? 1u : 0u) ||
         st->raw) {
-        for (uint32_t k = 0; k < ch.count; k++) status[ch.first + k] = TLSGPU_EMISMATCH;
+        for (uint32_t k = 0; k < cnt; k++) status[ch.first + k] = TLSGPU_EMISMATCH;
         return;
     }
     const bool stop = (ch.flags & TLSGPU_CHAIN_STOP_ON_ALERT) != 0;
     Rc4Stream dc;
     dc.load(st, lds);
     uint64_t seq = st->seqnum;
-    for (uint32_t k = 0; k < ch.count; k++) {
+    for (uint32_t k = 0; k < cnt; k++) {
         const tlsgpu_open_record R = recs[ch.first + k];
         const uint8_t* Cb = wire + R.ct_off;
         uint8_t* Pb = pt + R.pt_off;
         const uint32_t len = R.ct_len;
+        if (!in_arena(R.ct_off, len, wire_cap) || !in_arena(R.pt_off, len, pt_cap)) {
+            status[ch.first + k] = TLSGPU_EINVAL;  // outside the caller's arenas: not opened, state untouched
+            continue;
+        }
         bool macGood = true;
         uint32_t n = 0;
         if ((uint32_t)DL > len) {  // :1006-1007
@@ -267,7 +284,7 @@ __global__ void __launch_bounds__(SEAL_BLOCK) rc4_open_kernel(const tlsgpu_chain
         const int32_t res = macGood ? (int32_t)n : TLSGPU_ALERT_BAD_RECORD_MAC;
         status[ch.first + k] = res;
         if (stop && res < 0) {
-            for (uint32_t j = k + 1; j < ch.count; j++) status[ch.first + j] = TLSGPU_ALERT_SKIPPED;
+            for (uint32_t j = k + 1; j < cnt; j++) status[ch.first + j] = TLSGPU_ALERT_SKIPPED;
             break;
         }
     }
@@ -323,12 +340,13 @@ static uint32_t cu_count(hipStream_t s) {
 
 template <int MAC, bool SSL3>
 static hipError_t launch_rc4_open(const tlsgpu_chain* chains, uint32_t n, const tlsgpu_open_record* recs,
-                                  const uint8_t* wire, uint8_t* pt, ConnState* states, int32_t* status, hipStream_t s) {
+                                  uint32_t nrecords, const uint8_t* wire, uint8_t* pt, ConnState* states,
+                                  int32_t* status, hipStream_t s, const Bounds& b) {
     auto kern = rc4_open_kernel<MAC, SSL3>;
     hipError_t e = set_lds(kern, RC4_LDS_BYTES, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((n + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), RC4_LDS_BYTES, s, chains, n, recs,
-                       wire, pt, states, status);
+                       wire, pt, states, status, nrecords, b.wire_cap, b.pt_cap, b.nstates);
     return hipGetLastError();
 }
 
@@ -361,24 +379,16 @@ __global__ void fill_kernel(uint8_t* __restrict__ p, size_t bytes, uint64_t seed
 size_t seal_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * (sizeof(RecMeta) + TAIL_SLOT); }
 
 // AES batches with more chains than one generation of 16-wave cipher workgroups: the
-// many-chains configuration (C3_WAVES_MANY cipher waves, MAC kernel at MAC_LB_MANY)
+// many-chains configuration (the pair kernel with CFG_PAIR_GM-block groups, MAC kernel at MAC_LB_MANY)
 static bool many_chains(uint32_t nchains, hipStream_t s) {
-#ifdef TG_AB_NO_MANY
-    return false;
-#else
     return nchains > (uint32_t)C3_CHAINS * cu_count(s);
-#endif
 }
 
 // The AES cipher phase runs 2 lanes per chain (cbc_pair_kernel) when every CU gets at
 // least a full workgroup of chains (C3_CHAINS = 256: cfg2, cfg3), the quad layout
 // (cbc_kernel, latency form) with fewer (cfg4's 2-16 chains per CU).
 static bool pair_regime(uint32_t nchains, hipStream_t s) {
-#ifdef TG_AB_NO_PAIR
-    return false;
-#else
     return nchains >= (uint32_t)C3_CHAINS * cu_count(s);
-#endif
 }
 
 // phase 1 (stream s1): meta memset + seqnum prefix + per-record MAC / tail / header.
@@ -387,7 +397,7 @@ template <int NR, int MAC, bool SSL3>
 static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
                                    int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s,
-                                   const SealBounds& sb) {
+                                   const Bounds& sb) {
     constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
     constexpr int BS = NR == 0 ? 8 : 16;
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
@@ -399,13 +409,9 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
     hipError_t e = hipMemsetAsync(meta + r0, 0, (size_t)(r1 - r0) * sizeof(RecMeta), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((prefix_kernel<CID, MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains,
-                       recs, states, wire_len, meta, nrecords, epoch, sb.wire_cap);
+                       recs, states, wire_len, meta, nrecords, epoch, sb.pt_cap, sb.wire_cap, sb.nstates);
     const dim3 grid((r1 - r0 + 255) / 256);
-#ifdef TG_AB_PAIR_MAC_MANY
-    const bool mac_many = NR != 0 && nchains >= (uint32_t)C3_CHAINS * cu_count(s);
-#else
     const bool mac_many = NR != 0 && many_chains(nchains, s);
-#endif
     // (many chains: two 128-VGPR MAC waves per SIMD fit beside the cipher waves; beside the
     // two 88-VGPR pair waves the 168-VGPR kernel would fit two too -- measured the same on
     // cfg3, profiles/r03/ab_mac.txt)
@@ -418,57 +424,11 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
     return hipGetLastError();
 }
 
-// TG_AB_FUSED (A/B builds only): the AES seal in one kernel (tg_fused.h) in the pair regime,
-// the cipher's and the MAC's reads of the plaintext one.  Measured slower than the split
-// pipeline (cfg2 870 vs 965 GiB/s, cfg3 469 vs 558, same box), so the product
-// runs the split prefix / MAC / cbc_pair_kernel path there.
-static bool fused_regime(uint32_t nchains, hipStream_t s) {
-#ifdef TG_AB_FUSED
-    return pair_regime(nchains, s);
-#else
-    (void)nchains;
-    (void)s;
-    return false;
-#endif
-}
-#ifndef TG_AB_FUSED_G
-#define TG_AB_FUSED_G 8
-#endif
-#ifndef TG_AB_FUSED_GM
-#define TG_AB_FUSED_GM 8
-#endif
-
-#ifdef TG_AB_FUSED
-template <int NR, int MAC, bool SSL3>
-static hipError_t launch_fused(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
-                               uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
-                               int32_t* wire_len, uint64_t wire_cap, hipStream_t s) {
-    const uint32_t ncu = cu_count(s);
-    uint32_t cpw = (nchains + ncu - 1) / ncu;
-    cpw = cpw > (uint32_t)FZ_SLOTS ? (uint32_t)FZ_SLOTS : cpw;
-    uint32_t grid = (nchains + cpw - 1) / cpw;
-    grid = grid > ncu ? ncu : grid;
-    const bool many = many_chains(nchains, s);
-    auto kern = many ? seal_fused_kernel<NR, MAC, SSL3, TG_AB_FUSED_GM> : seal_fused_kernel<NR, MAC, SSL3, TG_AB_FUSED_G>;
-    hipError_t e = set_lds(kern, FZ_LDS_BYTES, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(FZ_THREADS), FZ_LDS_BYTES, s, chains, nchains, recs, nrecords, pt, wire,
-                       states, wire_len, cpw, wire_cap);
-    return hipGetLastError();
-}
-#else
-template <int NR, int MAC, bool SSL3>
-static hipError_t launch_fused(const tlsgpu_chain*, uint32_t, const tlsgpu_record*, uint32_t, const uint8_t*, uint8_t*,
-                               ConnState*, int32_t*, uint64_t, hipStream_t) {
-    return hipErrorInvalidDeviceFunction;  // never called: fused_regime() is false in the product
-}
-#endif
-
 // phase 2 (stream s2, after phase 1): CBC over [explicit IV | P blocks | tail]
 template <int NR>
 static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
-                                   uint8_t* ws, uint32_t epoch, hipStream_t s) {
+                                   uint8_t* ws, uint32_t epoch, hipStream_t s, uint32_t nstates) {
     const uint32_t ncu = cu_count(s);
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
@@ -478,7 +438,7 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         hipError_t e = set_lds(tdes4_kernel, D4_LDS_BYTES, s);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(tdes4_kernel, dim3((nchains + pw - 1) / pw), dim3(D4_THREADS), D4_LDS_BYTES, s, chains,
-                           nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch);
+                           nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch, nstates);
         return hipGetLastError();
     } else {
         const bool many = many_chains(nchains, s);
@@ -488,29 +448,28 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
             const uint32_t pwg = 32u * waves;
             uint32_t cpw = (nchains + ncu - 1) / ncu;
             cpw = cpw > pwg ? pwg : cpw;
-            auto kern = many ? cbc_pair_kernel<NR, PAIR_WAVES_MANY, TG_AB_PAIR_GM>
-                             : cbc_pair_kernel<NR, PAIR_WAVES, TG_AB_PAIR_G1>;
+            auto kern = many ? cbc_pair_kernel<NR, PAIR_WAVES_MANY, CFG_PAIR_GM>
+                             : cbc_pair_kernel<NR, PAIR_WAVES, CFG_PAIR_G1>;
             hipError_t e = set_lds(kern, AES_LDS_BYTES, s);
             if (e != hipSuccess) return e;
             uint32_t grid = (nchains + cpw - 1) / cpw;
             grid = grid > ncu ? ncu : grid;
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), AES_LDS_BYTES, s, chains, nchains, recs,
-                               nrecords, pt, wire, states, meta, tails, cpw, epoch);
+                               nrecords, pt, wire, states, meta, tails, cpw, epoch, nstates);
             return hipGetLastError();
         }
-        const uint32_t wg_chains = many ? 16u * C3_WAVES_MANY : (uint32_t)C3_CHAINS;
+        // fewer chains than the pair regime's (so at most one generation of C3_CHAINS per CU)
         uint32_t cpw = (nchains + ncu - 1) / ncu;
-        cpw = cpw < 1 ? 1 : (cpw > wg_chains ? wg_chains : cpw);
+        cpw = cpw < 1 ? 1 : (cpw > (uint32_t)C3_CHAINS ? (uint32_t)C3_CHAINS : cpw);
         // fewer chains than a workgroup's quads: the latency form of the AES round
-        auto kern = many ? cbc_kernel<NR, false, C3_WAVES_MANY>
-                         : cpw < (uint32_t)C3_CHAINS ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
+        auto kern = cpw < (uint32_t)C3_CHAINS ? cbc_kernel<NR, true> : cbc_kernel<NR, false>;
         hipError_t e = set_lds(kern, AES_LDS_BYTES, s);
         if (e != hipSuccess) return e;
         // persistent: at most one workgroup per CU, quads loop over chain generations
         uint32_t grid = (nchains + cpw - 1) / cpw;
         grid = grid > ncu ? ncu : grid;
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(many ? 64 * C3_WAVES_MANY : C3_THREADS), AES_LDS_BYTES, s, chains,
-                           nchains, recs, nrecords, pt, wire, states, meta, tails, cpw, epoch);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(C3_THREADS), AES_LDS_BYTES, s, chains,
+                           nchains, recs, nrecords, pt, wire, states, meta, tails, cpw, epoch, nstates);
         return hipGetLastError();
     }
 }
@@ -526,20 +485,13 @@ std::string seal_cipher_kernel(uint32_t variant, uint32_t nchains) {
     const uint32_t ncu = cu_count(nullptr);
     const bool many = many_chains(nchains, nullptr);
     char b[64];
-    if (fused_regime(nchains, nullptr)) {
-        const uint32_t m = (variant >> 8) & 0xff, ssl3 = (variant >> 16) & 1;
-        snprintf(b, sizeof b, "seal_fused_kernel<%d, %u, %s, %d>", nr, m, ssl3 ? "true" : "false",
-                 many ? TG_AB_FUSED_GM : TG_AB_FUSED_G);
-        return b;
-    }
     if (pair_regime(nchains, nullptr)) {
         snprintf(b, sizeof b, "cbc_pair_kernel<%d, %d, %d>", nr, many ? PAIR_WAVES_MANY : PAIR_WAVES,
-                 many ? TG_AB_PAIR_GM : TG_AB_PAIR_G1);
+                 many ? CFG_PAIR_GM : CFG_PAIR_G1);
         return b;
     }
     const uint32_t cpw = (nchains + ncu - 1) / ncu;
-    if (many) snprintf(b, sizeof b, "cbc_kernel<%d, false, %d>", nr, C3_WAVES_MANY);
-    else snprintf(b, sizeof b, "cbc_kernel<%d, %s>", nr, cpw < (uint32_t)C3_CHAINS ? "true" : "false");
+    snprintf(b, sizeof b, "cbc_kernel<%d, %s>", nr, cpw < (uint32_t)C3_CHAINS ? "true" : "false");
     return b;
 }
 
@@ -559,22 +511,10 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
                               const tlsgpu_record* recs, uint32_t nrecords, const uint8_t* pt, uint8_t* wire,
                               ConnState* states, int32_t* wire_len, uint8_t* ws, uint32_t epoch, hipStream_t s1,
                               hipEvent_t mac_done, hipStream_t s2, hipEvent_t cbc_start, hipEvent_t cbc_stop,
-                              bool* known, const SealBounds& sb) {
+                              bool* known, const Bounds& sb) {
     *known = true;
     hipError_t e = hipSuccess;
 #define TG_PH(CID, NR, MAC_ID, SSL3)                                                                            \
-    if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3) && NR != 0 && fused_regime(nchains, s2)) {                  \
-        /* one kernel on the cipher stream, ordered after whatever s1 waits for (host pipeline: H2D) */          \
-        if (s2 != s1) {                                                                                          \
-            if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                      \
-            if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                               \
-        }                                                                                                        \
-        if (cbc_start && (e = hipEventRecord(cbc_start, s2)) != hipSuccess) return e;                           \
-        e = launch_fused<NR == 0 ? 10 : NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states,      \
-                                                         wire_len, sb.wire_cap, s2);                             \
-        if (e == hipSuccess && cbc_stop) e = hipEventRecord(cbc_stop, s2);                                       \
-        return e;                                                                                                \
-    }                                                                                                            \
     if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3)) {                                                          \
         e = launch_mac_phase<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws,   \
                                                epoch, s1, sb);                                                   \
@@ -584,7 +524,7 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
             if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                               \
         }                                                                                                        \
         if (cbc_start && (e = hipEventRecord(cbc_start, s2)) != hipSuccess) return e;                           \
-        e = launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s2);              \
+        e = launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s2, sb.nstates);  \
         if (e == hipSuccess && cbc_stop) e = hipEventRecord(cbc_stop, s2);                                       \
         return e;                                                                                                \
     }
@@ -596,13 +536,13 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
 
 template <int MAC, bool SSL3>
 static hipError_t launch_rc4_seal(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
-                                  const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
-                                  hipStream_t s) {
+                                  uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
+                                  int32_t* wire_len, hipStream_t s, const Bounds& b) {
     auto kern = rc4_seal_kernel<MAC, SSL3>;
     hipError_t e = set_lds(kern, RC4_LDS_BYTES, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((nchains + SEAL_BLOCK - 1) / SEAL_BLOCK), dim3(SEAL_BLOCK), RC4_LDS_BYTES, s, chains,
-                       nchains, recs, pt, wire, states, wire_len);
+                       nchains, recs, pt, wire, states, wire_len, nrecords, b.pt_cap, b.wire_cap, b.nstates);
     return hipGetLastError();
 }
 
@@ -613,14 +553,14 @@ bool seal_needs_workspace(uint32_t variant) {
 
 hipError_t launch_seal(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                        uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states, int32_t* wire_len,
-                       uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known) {
+                       uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known, const Bounds& b) {
     if (seal_needs_workspace(variant))
         return launch_seal_phases(variant, chains, nchains, recs, nrecords, pt, wire, states, wire_len, ws, epoch, s,
-                                  nullptr, s, nullptr, nullptr, known);
+                                  nullptr, s, nullptr, nullptr, known, b);
     *known = true;
 #define TG_RC4_CASE(MAC_ID, SSL3)                       \
     if (variant == TLSGPU_VARIANT(TLSGPU_CIPHER_RC4, MAC_ID, SSL3)) \
-        return launch_rc4_seal<MAC_ID, SSL3>(chains, nchains, recs, pt, wire, states, wire_len, s);
+        return launch_rc4_seal<MAC_ID, SSL3>(chains, nchains, recs, nrecords, pt, wire, states, wire_len, s, b);
     TG_RC4_CASE(TLSGPU_MAC_SHA1, false)
     TG_RC4_CASE(TLSGPU_MAC_MD5, false)
     TG_RC4_CASE(TLSGPU_MAC_SHA1, true)
@@ -692,7 +632,10 @@ bool open_needs_workspace(uint32_t variant) { return open_split_variant(variant)
 // priority other than the caller's stream so the two never share a hardware queue (a shared
 // queue runs its kernels in submission order: no overlap), with the events
 // that order the parts.  Enqueueing holds the mutex: calls from several host threads
-// serialise their (microsecond) enqueue, and the events are reused only under it.
+// serialise their (microsecond) enqueue, and the events are reused only under it.  Limits
+// (tlsgpu.h): split opens issued on different caller streams of one priority share this
+// stream, so their decrypt passes run one after another; and a caller stream under HIP graph
+// capture pulls it into the capture.  tlsgpu_release_workspaces() destroys them.
 constexpr int OPEN_PARTS = 4;
 struct OpenAux {
     hipStream_t s2 = nullptr;
@@ -700,8 +643,8 @@ struct OpenAux {
     hipEvent_t dec_done[OPEN_PARTS] = {};
 };
 static std::mutex open_aux_mu;
+static std::map<std::pair<int, int>, OpenAux> open_aux_map;
 static hipError_t open_aux(hipStream_t s, OpenAux** out) {
-    static std::map<std::pair<int, int>, OpenAux> aux;
     const int dev = stream_device(s);
     int least = 0, greatest = 0, p = 0;
     DeviceGuard guard(dev);
@@ -709,7 +652,7 @@ static hipError_t open_aux(hipStream_t s, OpenAux** out) {
     if (e != hipSuccess) return e;
     if ((e = hipStreamGetPriority(s, &p)) != hipSuccess) return e;
     const int prio = p == greatest ? least : greatest;
-    OpenAux& a = aux[{dev, prio}];
+    OpenAux& a = open_aux_map[{dev, prio}];
     if (!a.s2) {
         if ((e = hipStreamCreateWithPriority(&a.s2, hipStreamNonBlocking, prio)) != hipSuccess) return e;
         for (auto& ev : a.dec_done)
@@ -720,6 +663,39 @@ static hipError_t open_aux(hipStream_t s, OpenAux** out) {
     return hipSuccess;
 }
 
+// the split open's library streams and events (tlsgpu_release_workspaces): each stream is
+// drained first; every entry is dropped even when a call fails (the first error is returned)
+hipError_t release_open_aux() {
+    std::lock_guard<std::mutex> g(open_aux_mu);
+    hipError_t first = hipSuccess;
+    auto keep = [&first](hipError_t e) {
+        if (e != hipSuccess && first == hipSuccess) first = e;
+    };
+    for (auto& kv : open_aux_map) {
+        DeviceGuard guard(kv.first.first);
+        OpenAux& a = kv.second;
+        if (a.s2) {
+            keep(hipStreamSynchronize(a.s2));
+            keep(hipStreamDestroy(a.s2));
+        }
+        for (auto& ev : a.dec_done)
+            if (ev) keep(hipEventDestroy(ev));
+        if (a.pre_done) keep(hipEventDestroy(a.pre_done));
+    }
+    open_aux_map.clear();
+    return first;
+}
+
+size_t open_aux_count() {
+    std::lock_guard<std::mutex> g(open_aux_mu);
+    return open_aux_map.size();
+}
+
+// The record threshold of the split open (tlsgpu_set_open_parts_min_records; the tests lower
+// it to run the parts path on small batches): -1 = the default, OPEN_PARTS * 512 per CU.
+static std::atomic<long long> open_parts_min{-1};
+void set_open_parts_min_records(long long n) { open_parts_min.store(n < 0 ? -1 : n, std::memory_order_relaxed); }
+
 // NR 0 = 3DES (8-byte blocks, open_tdes_kernel).  Large batches of short chains run in
 // OPEN_PARTS parts by chain range: decrypt + padding pass of part h on the second stream,
 // the MAC pass of part h on the caller's stream once they are done, beside the decrypt of
@@ -728,14 +704,14 @@ static hipError_t open_aux(hipStream_t s, OpenAux** out) {
 template <int NR, int MAC, bool SSL3>
 static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* recs,
                                     uint32_t nrecords, const uint8_t* wire, uint8_t* pt, ConnState* states,
-                                    int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s) {
+                                    int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, const Bounds& b) {
     constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
     OpenMeta* meta = reinterpret_cast<OpenMeta*>(ws);
     hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(OpenMeta), s);
     if (e != hipSuccess) return e;
     const dim3 gc((nchains + 255) / 256), gr((nrecords + 255) / 256);
     hipLaunchKernelGGL((open_prefix_kernel<CID, MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords,
-                       wire, states, status, meta, epoch);
+                       wire, states, status, meta, epoch, b.wire_cap, b.pt_cap, b.nstates);
     constexpr uint32_t WPB = (NR == 0 ? OT_THREADS : O3_THREADS) / 64;  // records per decrypt workgroup step
     const uint32_t ncu = cu_count(s);
     if (NR == 0) {
@@ -754,25 +730,21 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
             hipLaunchKernelGGL(open_aes_kernel<NR == 0 ? 10 : NR>, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s,
                                recs, nrecords, wire, pt, states, meta, epoch, c0, c1);
         hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), dim3((c1 - c0 + 255) / 256), dim3(256), 0, s, chains, nchains,
-                           recs, nrecords, pt, states, status, meta, epoch, c0, c1);
+                           recs, nrecords, pt, states, status, meta, epoch, c0, c1, b.nstates);
     };
-#ifdef TG_AB_OPEN_NOSPLIT
-    const bool parts = false;  // A/B: every pass once on the caller's stream
-#else
     // parts only when each part's MAC pass alone holds two waves per SIMD (one lane per
     // record): with fewer records a part's MAC takes as long as the whole batch's (its lanes
     // each hash a whole record), and four of them in a row lose (cfg2: 535-543 vs 733 GiB/s,
     // cfg5 198 vs 221; cfg3, 1 Mi records: 452 vs 402)
-    // (TLSGPU_OPEN_PARTS_MIN_RECORDS overrides the record threshold: the tests run the split
-    // path on batches of a few thousand records)
-    const char* env = getenv("TLSGPU_OPEN_PARTS_MIN_RECORDS");
-    const uint64_t min_rec = env ? strtoull(env, nullptr, 10) : (uint64_t)OPEN_PARTS * 512u * ncu;
+    // (tlsgpu_set_open_parts_min_records overrides the record threshold: the tests run the
+    // split path on batches of a few thousand records)
+    const long long set_min = open_parts_min.load(std::memory_order_relaxed);
+    const uint64_t min_rec = set_min >= 0 ? (uint64_t)set_min : (uint64_t)OPEN_PARTS * 512u * ncu;
     // and only for short chains (<= 4 records per chain on average): a part's padding pass
     // walks each chain's records one dependent load after another, and with long chains
     // (cfg4: 256 records) four of them in the decrypt stream plus the MAC waves holding the
     // CUs the next decrypt needs lose (cfg4 587-591 vs 668 GiB/s)
     const bool parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= min_rec && nrecords <= 4ull * nchains;
-#endif
     if (!parts) {
         dec_part(0, nchains, nrecords, s);
         hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status, meta,
@@ -804,12 +776,13 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
 
 hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
                        const tlsgpu_open_record* recs, uint32_t nrecords, const uint8_t* wire, uint8_t* pt,
-                       ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known) {
+                       ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known,
+                       const Bounds& b) {
     *known = true;
 #define TG_OPEN3(CID, NR, MAC_ID, SSL3)                                                                         \
     if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3))                                                           \
         return launch_open_split<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, wire, pt, states, status, ws, \
-                                                    epoch, s);
+                                                    epoch, s, b);
     TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)
     TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, false)
     TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA256, false)
@@ -821,7 +794,7 @@ hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nc
 #undef TG_OPEN3
 #define TG_OPEN_RC4(MAC_ID, SSL3)                                      \
     if (variant == TLSGPU_VARIANT(TLSGPU_CIPHER_RC4, MAC_ID, SSL3)) \
-        return launch_rc4_open<MAC_ID, SSL3>(chains, nchains, recs, wire, pt, states, status, s);
+        return launch_rc4_open<MAC_ID, SSL3>(chains, nchains, recs, nrecords, wire, pt, states, status, s, b);
     TG_OPEN_RC4(TLSGPU_MAC_SHA1, false)
     TG_OPEN_RC4(TLSGPU_MAC_MD5, false)
     TG_OPEN_RC4(TLSGPU_MAC_SHA1, true)

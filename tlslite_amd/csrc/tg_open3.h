@@ -27,8 +27,8 @@
 // Workspace per record: one 48-byte OpenMeta.
 //
 // A large open runs in parts by chain range (launch_open_split): the decrypt and
-// padding pass of part h+1 on the caller's stream beside the MAC pass of part h on a
-// second stream -- the decrypt is LDS-bound, the MAC VALU-bound.  Each kernel after
+// padding pass of part h+1 on the library's second stream beside the MAC pass of part h
+// on the caller's stream -- the decrypt is LDS-bound, the MAC VALU-bound.  Each kernel after
 // the prefix takes the part's chain range [c_lo, c_hi) and skips records of other
 // chains (OpenMeta.chain).
 #pragma once
@@ -72,18 +72,29 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
                                                          const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
                                                          const uint8_t* __restrict__ wire,
                                                          ConnState* __restrict__ states, int32_t* __restrict__ status,
-                                                         OpenMeta* __restrict__ meta, uint32_t epoch) {
+                                                         OpenMeta* __restrict__ meta, uint32_t epoch,
+                                                         uint64_t wire_cap, uint64_t pt_cap, uint32_t nstates) {
     const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
-    ConnState* st = states + ch.state;
+    // a state index outside the caller's array: every record refused, no state read (ABI 6)
+    const bool sok = ch.state < nstates;
+    ConnState* st = states + (sok ? ch.state : 0u);
     // state header without short-circuit branches (one memory latency, as prefix_kernel)
-    const uint4 h0 = *(const uint4*)st;                         // cipher, mac, vmaj..maclen, ssl3
-    const uint4 h1 = *(const uint4*)((const uint8_t*)st + 16);  // seqnum (lo, hi), explicit_iv, raw
-    const bool ok = (h0.x == (uint32_t)CIPHER_ID) & (h0.y == (uint32_t)MAC) & (h0.w == (SSL3 ? 1u : 0u)) & (h1.w == 0u);
+    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = make_uint4(0, 0, 0, 0);
+    uint32_t res[4] = {0, 0, 0, 0};
     constexpr uint32_t BS = CIPHER_ID == TLSGPU_CIPHER_3DES ? 8u : 16u;
+    if (sok) {
+        h0 = *(const uint4*)st;                         // cipher, mac, vmaj..maclen, ssl3
+        h1 = *(const uint4*)((const uint8_t*)st + 16);  // seqnum (lo, hi), explicit_iv, raw
+        res[0] = st->iv[0];
+        res[1] = st->iv[1];
+        res[2] = BS == 16 ? st->iv[2] : 0u;
+        res[3] = BS == 16 ? st->iv[3] : 0u;
+    }
+    const bool ok = sok & (h0.x == (uint32_t)CIPHER_ID) & (h0.y == (uint32_t)MAC) & (h0.w == (SSL3 ? 1u : 0u)) &
+                    (h1.w == 0u);
     const uint32_t E = h1.z ? BS : 0u;
-    uint32_t res[4] = {st->iv[0], st->iv[1], BS == 16 ? st->iv[2] : 0u, BS == 16 ? st->iv[3] : 0u};
     for (uint32_t k = 0; k < ch.count; k++) {
         const uint32_t r = ch.first + k;
         if (r >= nrecords) break;
@@ -98,11 +109,16 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
         m.n = 0;
         m.chain = cid;
         if (!ok) {
-            status[r] = TLSGPU_EMISMATCH;
+            status[r] = sok ? TLSGPU_EMISMATCH : TLSGPU_EINVAL;
         } else {
             const tlsgpu_open_record R = recs[r];
             const uint32_t L = R.ct_len;
-            if (L & (BS - 1)) {  // :964-968 -- not decrypted, residue unchanged
+            if (!in_arena(R.ct_off, L, wire_cap) || !in_arena(R.pt_off, L > E ? L - E : 0u, pt_cap)) {
+                // outside the caller's arenas: not opened, nothing written, residue and seqnum as
+                // if the record were not in the batch
+                status[r] = TLSGPU_EINVAL;
+                m.epoch = 0;  // no later pass of this launch looks at it (open_seq_kernel: no seqnum)
+            } else if (L & (BS - 1)) {  // :964-968 -- not decrypted, residue unchanged
                 status[r] = TLSGPU_ALERT_DECRYPTION_FAILED;
             } else {
                 if (L) {  // decrypt() keeps the last block
@@ -307,11 +323,12 @@ __global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __res
                                                       const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
                                                       const uint8_t* __restrict__ pt, ConnState* __restrict__ states,
                                                       int32_t* __restrict__ status, OpenMeta* __restrict__ meta,
-                                                      uint32_t epoch, uint32_t c_lo, uint32_t c_hi) {
+                                                      uint32_t epoch, uint32_t c_lo, uint32_t c_hi, uint32_t nstates) {
     constexpr uint32_t DL = Hash<MAC>::DLEN;
     const uint32_t cid = c_lo + blockIdx.x * blockDim.x + threadIdx.x;  // chains [c_lo, c_hi) of nchains
     if (cid >= c_hi || cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
+    if (ch.state >= nstates) return;  // refused by open_prefix_kernel (ABI 6): no state read
     ConnState* st = states + ch.state;
     uint64_t seq = st->seqnum;
     bool any = false;

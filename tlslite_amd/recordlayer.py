@@ -123,14 +123,37 @@ def seal_cipher_kernel(variant, nchains):
     return buf.value.decode()
 
 
-def seal_dev(chains, nchains, records, nrecords, pt, wire, states, wire_len, variant, workspace=None, stream=None):
+def _p(x):
+    return x.ptr if isinstance(x, DeviceBuffer) else ctypes.c_void_p(x)
+
+
+def _size(x, given, what):
+    """An arena's byte size for the ABI-6 bounds: given explicitly, or the DeviceBuffer's."""
+    if given is not None:
+        return int(given)
+    if isinstance(x, DeviceBuffer):
+        return int(x.nbytes)
+    raise ValueError("%s is a raw address: pass its size (the library checks every record against it)" % what)
+
+
+def _nstates(states, nstates):
+    if nstates is not None:
+        return int(nstates)
+    if isinstance(states, DeviceBuffer):
+        return int(states.nbytes // STATE_BYTES)
+    raise ValueError("states is a raw address: pass nstates")
+
+
+def seal_dev(chains, nchains, records, nrecords, pt, wire, states, wire_len, variant, workspace=None, stream=None,
+             pt_bytes=None, wire_bytes=None, nstates=None):
     """Device-resident batch seal (all pointers are DeviceBuffer / addresses).
     workspace: DeviceBuffer of >= seal_workspace_bytes(nrecords), or None for
-    the library-owned one (then no concurrent calls on other streams)."""
-    def p(x):
-        return x.ptr if isinstance(x, DeviceBuffer) else ctypes.c_void_p(x)
-    N.call("tlsgpu_seal_dev", p(chains), nchains, p(records), int(nrecords), p(pt), p(wire), p(states), p(wire_len),
-           variant, None if workspace is None else p(workspace), 0 if workspace is None else workspace.nbytes,
+    the library-owned one (one per stream).  pt_bytes / wire_bytes / nstates: the
+    arenas' sizes and the state count (ABI 6 bounds; taken from DeviceBuffers when not
+    given): a record outside them gets wire_len = EINVAL and is not sealed."""
+    N.call("tlsgpu_seal_dev", _p(chains), nchains, _p(records), int(nrecords), _p(pt), _size(pt, pt_bytes, "pt"),
+           _p(wire), _size(wire, wire_bytes, "wire"), _p(states), _nstates(states, nstates), _p(wire_len),
+           variant, None if workspace is None else _p(workspace), 0 if workspace is None else workspace.nbytes,
            stream.handle if stream is not None else None)
 
 
@@ -147,11 +170,11 @@ class SealPipeline:
         self.max_records = int(max_records)
 
     def seal(self, chains, nchains, records, nrecords, pt, wire, states, wire_len, variant,
-             cipher_start=None, cipher_stop=None):
-        def p(x):
-            return x.ptr if isinstance(x, DeviceBuffer) else ctypes.c_void_p(x)
-        N.call("tlsgpu_pipeline_seal", self.handle, p(chains), nchains, p(records), int(nrecords), p(pt), p(wire),
-               p(states), p(wire_len), variant, cipher_start.handle if cipher_start is not None else None,
+             cipher_start=None, cipher_stop=None, pt_bytes=None, wire_bytes=None, nstates=None):
+        N.call("tlsgpu_pipeline_seal", self.handle, _p(chains), nchains, _p(records), int(nrecords), _p(pt),
+               _size(pt, pt_bytes, "pt"), _p(wire), _size(wire, wire_bytes, "wire"), _p(states),
+               _nstates(states, nstates), _p(wire_len), variant,
+               cipher_start.handle if cipher_start is not None else None,
                cipher_stop.handle if cipher_stop is not None else None)
 
     def synchronize(self):
@@ -182,12 +205,12 @@ class HostSealPipeline:
         N.call("tlsgpu_host_pipeline_create", ctypes.byref(h), int(chunk_bytes), int(depth))
         self.handle = h
 
-    def seal(self, chains, records, pt_host, wire_host, states, wire_len_host, variant):
+    def seal(self, chains, records, pt_host, wire_host, states, wire_len_host, variant, nstates=None):
         """chains / records: ctypes arrays (host); pt_host / wire_host: numpy uint8
         arrays (host); states: DeviceBuffer; wire_len_host: numpy int32 [nrecords]."""
         N.call("tlsgpu_host_pipeline_seal", self.handle, ctypes.addressof(chains), len(chains),
                ctypes.addressof(records), len(records), pt_host.ctypes.data_as(ctypes.c_void_p), pt_host.nbytes,
-               wire_host.ctypes.data_as(ctypes.c_void_p), wire_host.nbytes, states.ptr,
+               wire_host.ctypes.data_as(ctypes.c_void_p), wire_host.nbytes, states.ptr, _nstates(states, nstates),
                wire_len_host.ctypes.data_as(ctypes.c_void_p), variant)
 
     def close(self):
@@ -313,14 +336,21 @@ def open_workspace_bytes(nrecords):
     return int(N.lib.tlsgpu_open_workspace_bytes(int(nrecords)))
 
 
-def open_dev(chains, nchains, records, nrecords, wire, pt, states, status, variant, workspace=None, stream=None):
+def open_dev(chains, nchains, records, nrecords, wire, pt, states, status, variant, workspace=None, stream=None,
+             wire_bytes=None, pt_bytes=None, nstates=None):
     """Device-resident batch open (decrypt + padding + MAC check).  workspace:
-    DeviceBuffer of >= open_workspace_bytes(nrecords), or None (library-owned)."""
-    def p(x):
-        return x.ptr if isinstance(x, DeviceBuffer) else ctypes.c_void_p(x)
-    N.call("tlsgpu_open_dev", p(chains), nchains, p(records), int(nrecords), p(wire), p(pt), p(states), p(status),
-           variant, None if workspace is None else p(workspace), 0 if workspace is None else workspace.nbytes,
+    DeviceBuffer of >= open_workspace_bytes(nrecords), or None (library-owned).
+    wire_bytes / pt_bytes / nstates: ABI 6 bounds (from DeviceBuffers when not given)."""
+    N.call("tlsgpu_open_dev", _p(chains), nchains, _p(records), int(nrecords), _p(wire), _size(wire, wire_bytes, "wire"),
+           _p(pt), _size(pt, pt_bytes, "pt"), _p(states), _nstates(states, nstates), _p(status),
+           variant, None if workspace is None else _p(workspace), 0 if workspace is None else workspace.nbytes,
            stream.handle if stream is not None else None)
+
+
+def set_open_parts_min_records(n):
+    """Record count from which an open runs in parts (None / negative: the library default);
+    tests lower it to exercise the parts path on small batches."""
+    N.call("tlsgpu_set_open_parts_min_records", -1 if n is None else int(n))
 
 
 def open_records(states, records, stream=None, stop_on_alert=True):

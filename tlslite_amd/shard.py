@@ -10,9 +10,13 @@ done by a small TCP rendezvous of our own (no PyTorch, no RCCL): rank 0 serves
 MASTER_PORT itself -- (or `TLSGPU_RDZV_PORT`), every other rank connects, and
 each collective is an all-gather of byte strings through rank 0.
 
-A rank's hello carries a shared token (TLSGPU_RDZV_TOKEN, which bench.py's own rank
-spawner sets, else torch.distributed.run's TORCHELASTIC_RUN_ID): rank 0 drops
-connections that do not present it.  Sockets keep a finite timeout after set-up, so a
+A rank's hello carries a shared token (`job_token()`: TLSGPU_RDZV_TOKEN, which bench.py's
+own rank spawner sets to a random value; else torch.distributed.run's TORCHELASTIC_RUN_ID;
+torchrun sets that to the constant "none" unless --rdzv-id / --standalone is given, and then a
+single-node job's token is derived from MASTER_ADDR:MASTER_PORT and the launcher's PID, the
+parent of every local rank): rank 0 drops connections that do not present it.  The token
+keeps stray and foreign processes out; it is not authentication against a local process
+that reads the ranks' environment.  Sockets keep a finite timeout after set-up, so a
 rank that hangs ends the others with an error instead of blocking them forever."""
 import errno
 import os
@@ -54,6 +58,22 @@ def _recv(sock):
     return _recv_exact(sock, n)
 
 
+def job_token(env=None, ppid=None):
+    """The rendezvous token all ranks of one job share (module docstring)."""
+    env = os.environ if env is None else env
+    tok = env.get("TLSGPU_RDZV_TOKEN")
+    if tok:
+        return tok
+    run_id = env.get("TORCHELASTIC_RUN_ID") or ""
+    if run_id and run_id != "none":
+        return run_id
+    if run_id == "none" and env.get("LOCAL_WORLD_SIZE") and env.get("LOCAL_WORLD_SIZE") == env.get("WORLD_SIZE"):
+        # torch.distributed.run without --rdzv-id on one node: every rank is a child of the agent
+        return "%s:%s:%d" % (env.get("MASTER_ADDR", ""), env.get("MASTER_PORT", ""),
+                             os.getppid() if ppid is None else ppid)
+    return run_id
+
+
 class ShardGroup:
     """RANK / WORLD_SIZE / LOCAL_RANK / MASTER_ADDR / MASTER_PORT from the
     environment (as torch.distributed.run sets them); world size 1 needs none."""
@@ -68,7 +88,7 @@ class ShardGroup:
             return
         addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
         port = int(os.environ.get("TLSGPU_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
-        token = (os.environ.get("TLSGPU_RDZV_TOKEN") or os.environ.get("TORCHELASTIC_RUN_ID") or "").encode()[:255]
+        token = job_token().encode()[:255]
         deadline = time.monotonic() + timeout
         if self.rank == 0:
             srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)

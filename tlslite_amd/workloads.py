@@ -247,8 +247,9 @@ class Workload:
         for i, (var, d_ch, nch) in enumerate(self.launches):
             s = None if not streams else streams[i % len(streams)]
             ws = self.d_ws[i]
-            N.call("tlsgpu_seal_dev", d_ch.ptr, nch, self.d_recs.ptr, self.n_records, self.d_pt.ptr, self.d_wire.ptr,
-                   self.d_states.ptr, self.d_len.ptr, var, ws.ptr, ws.nbytes, s.handle if s else None)
+            N.call("tlsgpu_seal_dev", d_ch.ptr, nch, self.d_recs.ptr, self.n_records, self.d_pt.ptr, self.d_pt.nbytes,
+                   self.d_wire.ptr, self.d_wire.nbytes, self.d_states.ptr, self.d_states.nbytes // N.CONN_STATE_BYTES,
+                   self.d_len.ptr, var, ws.ptr, ws.nbytes, s.handle if s else None)
 
     # ------------------------------------------------------------ open direction
     def open_setup(self):

@@ -13,6 +13,8 @@
 #   torchrun2          the same two ranks under python -m torch.distributed.run
 #   prof=cfg           rocprofv3 --kernel-trace --stats of a 20-step bench run -> <tag>/prof_<cfg>
 #   pmc=cfg            tools/pmc_kernels.sh (one rocprofv3 --pmc pass per counter group)
+#   profopen=cfg       rocprofv3 --kernel-trace --stats of a short bench run with the open leg -> <tag>/profopen_<cfg>
+#   pmcopen=cfg        tools/pmc_kernels.sh with the open leg -> profiles/pmc_open_<cfg>.json
 #   ab=cfg:rounds:v1,v2,...   tools/ab_bench.sh (variant "base" = the product library)
 #   openab=cfg:rounds:v1,v2,... the open-path rate (bench's open leg, 20 + 5 seal steps) per
 #                      library build, same call ("base" = the product library)
@@ -94,6 +96,24 @@ for step in "$@"; do
         || { echo "STEP prof $c FAILED"; tail -20 $O/prof_$c.err; exit 1; }
       f=$(find $O/prof_$c -name "*kernel_stats.csv" | head -1)
       head -4 $f | cut -c1-200 ;;
+    profopen)
+      c=${arg:-cfg2}
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/profopen_$c -o run \
+          --output-format csv -- python3 $R/bench.py --config $c --no-cpu --no-check --no-derive --no-host-inclusive \
+          --steps 20 --warmup 5 > $O/profopen_$c.out 2> $O/profopen_$c.err ) \
+        || { echo "STEP profopen $c FAILED"; tail -20 $O/profopen_$c.err; exit 1; }
+      f=$(find $O/profopen_$c -name "*kernel_stats.csv" | head -1)
+      head -12 $f | cut -c1-160 ;;
+    pmcopen)
+      c=${arg:-cfg2}
+      PMC_NAME=pmc_open_$c timeout -k 10 1000 bash tools/pmc_kernels.sh $c $O/pmcopen_$c --open > $O/pmcopen_$c.log 2>&1 \
+        || { echo "STEP pmcopen $c FAILED"; tail -20 $O/pmcopen_$c.log; exit 1; }
+      cp $R/profiles/pmc_open_$c.json $O/pmc_open_$c.json
+      python3 -c "
+import json;d=json.load(open('$O/pmc_open_$c.json'))
+for k,v in d['kernels'].items():
+  if k.startswith('open_'): print(k, round(v.get('duration_ms',0),3), 'hbm', v.get('hbm_bytes'), 'lds_busy', v.get('lds_busy'), 'clk', v.get('clock_ghz'), 'conf', v.get('SQ_LDS_BANK_CONFLICT'), 'lds', v.get('SQ_INSTS_LDS'))
+print('open call', d.get('open_call_hbm_bytes'))" ;;
     pmc)
       c=${arg:-cfg2}
       timeout -k 10 1000 bash tools/pmc_kernels.sh $c $O/pmc_$c > $O/pmc_$c.log 2>&1 \

@@ -6,6 +6,8 @@
 # where FETCH_SIZE tallies 128-B requests at 64 B -- tools/traffic_calib.hip).  PMC
 # mode serialises dispatches, so every kernel is measured on its own.  Usage (GPU box):
 #   bash tools/pmc_kernels.sh <config> <outdir> [extra bench args]
+# PMC_NAME=<name>: write profiles/<name>.json (default pmc_<config>); with --open among the
+# extra args the open leg's kernels are counted too (open_call_hbm_bytes).
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 CFG=${1:-cfg2}
@@ -24,4 +26,4 @@ for G in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_
       python $R/bench.py --config $CFG --steps 3 --warmup 1 --no-check --no-cpu --no-host-inclusive --no-open --no-derive "$@" > $OUT/g$i.log 2>&1
   i=$((i+1))
 done
-python $R/tools/pmc_summarize.py $OUT $CFG
+python $R/tools/pmc_summarize.py $OUT $CFG ${PMC_NAME:-pmc_$CFG}

@@ -20,11 +20,13 @@ import statistics
 import sys
 
 out, cfg = sys.argv[1], sys.argv[2]
+name = sys.argv[3] if len(sys.argv) > 3 else "pmc_%s" % cfg  # profiles/<name>.json
 NCU = 256
 # bench set-up: synthetic plaintext fill, buffer zeroing, state resets and the copy-rate
 # measurement (d2d copies) -- not the seal call
 SETUP = ("fill_kernel", "__amd_rocclr_fillBuffer", "__amd_rocclr_copyBuffer")
-DOMINANT = ("seal_fused_kernel", "cbc_pair_kernel", "cbc_kernel", "rc4_seal_kernel", "tdes4_kernel")
+DOMINANT = ("cbc_pair_kernel", "cbc_kernel", "rc4_seal_kernel", "tdes4_kernel")
+OPEN = ("open_", "rc4_open_kernel")  # the open path's kernels (bench.py --open): summed apart
 
 
 def stem(name):
@@ -97,7 +99,8 @@ for k, cs in counters.items():
         row["valu_inst_per_simd_cycle"] = round(row.get("SQ_INSTS_VALU", 0) / (4 * NCU) / cyc, 4)
     res["kernels"][k] = row
 
-seal = {k: r for k, r in res["kernels"].items() if not k.startswith(SETUP)}
+seal = {k: r for k, r in res["kernels"].items() if not k.startswith(SETUP) and not k.startswith(OPEN)}
+opn = {k: r for k, r in res["kernels"].items() if k.startswith(OPEN)}
 dom = [k for k in seal if k.startswith(DOMINANT)]
 dom = max(dom, key=lambda k: seal[k].get("duration_ms", 0)) if dom else None
 res["dominant_kernel"] = dom
@@ -105,12 +108,14 @@ res["hbm_bytes_per_launch"] = seal[dom].get("hbm_bytes") if dom else None
 res["hbm_bytes_per_launch_raw"] = (int((seal[dom].get("FETCH_SIZE", 0) + seal[dom].get("WRITE_SIZE", 0)) * 1024)
                                    if dom else None)
 res["seal_call_hbm_bytes"] = sum(r.get("hbm_bytes", 0) for r in seal.values())
+if opn:
+    res["open_call_hbm_bytes"] = sum(r.get("hbm_bytes", 0) for r in opn.values())
 res["note"] = ("hbm_bytes_per_launch: the dominant kernel's HBM bytes per launch = reads from the "
                "request-size counters (32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B) + WRITE_SIZE*1024 "
                "(read_bytes_2xfetch: the FETCH_SIZE doubling, exact only for wide streaming reads); "
                "seal_call_hbm_bytes: sum over the seal call's kernels; set-up kernels (%s) excluded; "
                "clock = GRBM_GUI_ACTIVE / 8 XCDs / duration" % ", ".join(SETUP))
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-with open(os.path.join(root, "profiles", "pmc_%s.json" % cfg), "w") as fh:
+with open(os.path.join(root, "profiles", name + ".json"), "w") as fh:
     json.dump(res, fh, indent=1)
 print(json.dumps(res, indent=1))
