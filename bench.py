@@ -229,6 +229,30 @@ def oracle_check(wl, wire_gpu, nthreads, sample=None, min_seconds=0.0):
     return ok, dt, len(recs), int(wl.pt_len[recs].sum()) * reps, nthreads, reps
 
 
+def oracle_wire(wl, nthreads):
+    """The whole batch sealed by the CPU oracle from the initial states (wire arena)."""
+    from oracle import oracle as O
+    protos = oracle_protos(wl, np.arange(wl.n_chains))
+    pt = wl.host_plaintext(O.fill_pattern)
+    wire = np.zeros(wl.wire_bytes, dtype=np.uint8)
+    O.seal_batch(protos, wl.chain_first, wl.chain_count, pt, wl.pt_off, wl.pt_len, wire, wl.wire_off,
+                 nthreads=nthreads)
+    return wire
+
+
+def shard_parity(D, wl, wire_gpu, min_seconds=0.0):
+    """Every rank checks its WHOLE shard (the batch it sealed) against the CPU oracle, with
+    its share of the job's host cores (usable_cpus() // LOCAL_WORLD_SIZE); `bit_exact` is the
+    AND over the ranks (an all-gather of the per-rank results).  min_seconds > 0 (rank 0 at
+    N = 1) also times the oracle for cpu_baseline.  -> (bit_exact, per-rank results, threads,
+    oracle_check's timing tuple)."""
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", D.world) or 1)
+    nthreads = max(1, usable_cpus()[0] // max(1, local_world))
+    ok, dt, nrec, ptb, th, reps = oracle_check(wl, wire_gpu, nthreads, min_seconds=min_seconds)
+    oks = [bool(json.loads(b.decode())) for b in D.gather_bytes(json.dumps(bool(ok)).encode())]
+    return all(oks), oks, nthreads, (dt, nrec, ptb, th, reps)
+
+
 def pmc_traffic(path, workload, n_records, dominant):
     """(HBM bytes per launch of the dominant kernel, HBM bytes of one seal call) from a PMC
     summary (tools/pmc_kernels.sh -> profiles/pmc_<cfg>.json), only when it names this kernel
@@ -523,7 +547,11 @@ def spawn_ranks(args):
 
 
 def dry_run(args, D):
-    """--dry-run: the N-rank plumbing without the GPU (CPU tests of the spawner)."""
+    """--dry-run: the N-rank plumbing without the GPU (CPU tests of the spawner).  With
+    --records R every rank also runs the shard parity check (shard_parity) on an R-record
+    cfg2-shaped batch whose "GPU output" is the oracle's own wire arena -- one byte of it
+    flipped on the rank named by TLSGPU_DRYRUN_CORRUPT_RANK -- so the AND over ranks is
+    exercised without a GPU."""
     from tlslite_amd.shard import device_for_rank
     ndev = int(os.environ.get("TLSGPU_DRYRUN_DEVICES", max(D.world, 1)))
     if D.world > ndev and not args.share_devices:
@@ -533,9 +561,18 @@ def dry_run(args, D):
     me = {"rank": D.rank, "local_rank": D.local, "device": device_for_rank(D.local, ndev), "pid": os.getpid()}
     ranks = [json.loads(b) for b in D.gather_bytes(json.dumps(me).encode())]
     t = D.max(0.001 * (1 + D.rank))
+    parity = None
+    if args.records:
+        from tlslite_amd import workloads as W
+        wl = W.cfg2(n=int(args.records), pt_len=1500 + 16 * D.rank, seed=7 + D.rank)  # each rank its own batch
+        wire = oracle_wire(wl, 1)
+        if os.environ.get("TLSGPU_DRYRUN_CORRUPT_RANK") == str(D.rank):
+            wire[int(wl.wire_off[len(wl.wire_off) // 2]) + 9] ^= 0x40
+        ok, oks, nthreads, _ = shard_parity(D, wl, wire)
+        parity = {"bit_exact": ok, "bit_exact_ranks": oks, "threads_per_rank": nthreads}
     if D.rank == 0:
         print(json.dumps({"metric": "dry-run", "n_gpus": D.world, "ranks": ranks, "t_max": t,
-                          "devices_shared": D.world > ndev}))
+                          "devices_shared": D.world > ndev, "parity": parity}))
     D.close()
 
 
@@ -572,15 +609,16 @@ def main():
     wl.to_device(stream)
     stream.synchronize()
 
-    # ---- one launch for the parity check against the CPU oracle (full batch, rank 0 at N=1):
+    # ---- one launch for the parity check against the CPU oracle (every rank its full batch):
     # its output is parked in a second device buffer and downloaded, compared -- and the CPU
     # baseline timed -- after the timed region, so the GPU does not sit idle through the
     # download and seconds of CPU work right before it
     bit_exact = None
+    bit_exact_ranks = None
     cpu = None
     wire_gpu = None
     d_hold = None
-    if D.world == 1 and not args.no_check:
+    if not args.no_check:
         from tlslite_amd.device import DeviceBuffer
         d_hold = DeviceBuffer(wl.wire_bytes)
         wl.launch([stream])
@@ -674,12 +712,14 @@ def main():
         wire_gpu = d_hold.download()
         d_hold.free()
     if wire_gpu is not None:
-        nthreads, cpu_note = usable_cpus()
-        ok, dt, nrec, ptb, th, reps = oracle_check(wl, wire_gpu, nthreads,
-                                                   min_seconds=0.0 if args.no_cpu else args.cpu_seconds)
+        # every rank checks its whole shard (the AND over ranks is bit_exact); the CPU baseline
+        # is timed on rank 0 at N = 1 only
+        baseline = D.world == 1 and not args.no_cpu
+        bit_exact, bit_exact_ranks, _, (dt, nrec, ptb, th, reps) = shard_parity(
+            D, wl, wire_gpu, min_seconds=args.cpu_seconds if baseline else 0.0)
         del wire_gpu
-        bit_exact = ok
-        if not args.no_cpu:
+        cpu_note = usable_cpus()[1]
+        if baseline:
             cpu = {"value": round(ptb / GIB / dt, 4), "unit": "GiB/s", "cores": th,
                    "per_core": round(ptb / GIB / dt / th, 5), "kind": "port",
                    "sample": "full batch (%d records, %.1f MiB plaintext) sealed %d times in succession by "
@@ -780,6 +820,10 @@ def main():
             "ms_per_seal_call": round(call_ms, 4),
             "cpu_baseline": cpu,
             "bit_exact": bit_exact,
+            "bit_exact_ranks": bit_exact_ranks,
+            "bit_exact_check": "every rank's whole batch (as sealed by one tlsgpu_seal_dev call from the initial "
+                               "states) against the CPU oracle on its share of the host cores; bit_exact = AND "
+                               "over the ranks",
             "timed_bit_exact": timed_ok,
             "timed_check": "pipeline-vs-sequential consistency: the %d seals before the last step's output "
                            "replayed one tlsgpu_seal_dev call at a time from the initial states; last wire arena, "

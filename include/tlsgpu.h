@@ -323,8 +323,8 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain *chains
  * wire: ciphertext arena of wire_bytes, pt: plaintext arena of pt_bytes, states: nstates
  * states (ABI 6 bounds: a refused record gets status TLSGPU_EINVAL and is treated as if it
  * were not in the batch).
- * Large batches of short chains open in parts on a library-owned second stream beside the
- * caller's.  Limits of that stream: one per (device, priority), so
+ * Large batches open in parts on a library-owned second stream beside the caller's
+ * (DESIGN.md section 3.4).  Limits of that stream: one per (device, priority), so
  * split opens issued at once on different caller streams of one priority run their decrypt
  * passes one after another; and a caller stream under HIP graph capture pulls it into the
  * capture.  tlsgpu_release_workspaces destroys it. */
@@ -333,9 +333,13 @@ int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_o
                     uint32_t nrecords, const uint8_t *wire, size_t wire_bytes, uint8_t *pt, size_t pt_bytes,
                     tlsgpu_conn_state *states, uint32_t nstates, int32_t *status, uint32_t variant,
                     void *workspace, size_t workspace_bytes, tlsgpu_stream s);
-/* ABI 6: the record count from which an open runs in parts (n < 0: the library's default,
- * 4 parts x 512 records per CU); tests lower it to exercise the parts path.  Process-wide. */
-int tlsgpu_set_open_parts_min_records(int64_t n);
+/* ABI 6: how CBC-suite opens are split (process-wide).
+ * mode TLSGPU_OPEN_SPLIT_AUTO (the default): the library picks from the batch shape;
+ * CHAINS / BLOCKS: that form for every batch of at least min_records records (tests);
+ * NONE: every pass once on the caller's stream. */
+enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_BLOCKS = 2,
+       TLSGPU_OPEN_SPLIT_NONE = 3 };
+int tlsgpu_set_open_parts(int mode, int64_t min_records);
 /* raw stateful encrypt (decrypt=0) / decrypt (decrypt=1) of spans; one span
  * per state per launch (a state's spans in one launch run in array order). */
 int tlsgpu_cipher_dev(const tlsgpu_span *spans, uint32_t nspans, const uint8_t *in, uint8_t *out,

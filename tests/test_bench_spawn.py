@@ -55,3 +55,19 @@ def test_single_gpu_needs_no_spawn():
     assert r.returncode == 0, r.stderr[-2000:]
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert d["n_gpus"] == 1 and d["ranks"][0]["pid"] != os.getpid()
+
+
+def test_dry_run_parity_is_reduced_over_ranks():
+    """bench.py's N > 1 parity: every rank checks its whole shard
+    against the CPU oracle (shard_parity, its share of the host cores) and bit_exact is
+    the AND over the ranks.  --dry-run --records R stands the oracle's own output in for
+    the GPU's; a byte flipped on one rank must turn rank 0's bit_exact false."""
+    r = _run(["--gpus", "3", "--dry-run", "--records", "48"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    p = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])["parity"]
+    assert p["bit_exact"] is True and p["bit_exact_ranks"] == [True, True, True]
+    assert p["threads_per_rank"] >= 1
+    r = _run(["--gpus", "3", "--dry-run", "--records", "48"], TLSGPU_DRYRUN_CORRUPT_RANK="2")
+    assert r.returncode == 0, r.stderr[-2000:]
+    p = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])["parity"]
+    assert p["bit_exact"] is False and p["bit_exact_ranks"] == [True, True, False]

@@ -270,33 +270,41 @@ def test_stop_on_alert_like_connection(suite, version):
             assert r.iv == o.iv
 
 
-@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES256-SHA256", (3, 3)), ("3DES-SHA", (3, 1)),
-                                           ("AES128-SHA", (3, 0))])
-def test_split_open_parts_like_oracle(suite, version):
-    """The open in parts (launch_open_split: decrypt and padding pass of chain range h+1 on
-    a second stream beside the MAC pass of range h; the library does this from 512 records
-    per CU per part, tlsgpu_set_open_parts_min_records lowers the threshold here):
-    6,000 connections of 1-6 records of 1-700 B, ~3 % of records tampered or
-    truncated, connection (stop-on-alert) semantics -- every status, plaintext and final
-    state equals the oracle's, across the part boundaries (tlsrecordlayer.py:958-1044)."""
+@pytest.mark.parametrize("suite,version,mode", [("AES128-SHA", (3, 3), "chains"), ("AES256-SHA256", (3, 3), "chains"),
+                                                ("3DES-SHA", (3, 1), "chains"), ("AES128-SHA", (3, 0), "chains"),
+                                                ("AES128-SHA", (3, 3), "blocks"), ("AES256-SHA256", (3, 3), "blocks"),
+                                                ("3DES-SHA", (3, 2), "blocks"), ("AES128-SHA", (3, 0), "blocks"),
+                                                ("AES256-SHA", (3, 1), "blocks")])
+def test_split_open_parts_like_oracle(suite, version, mode):
+    """The open in parts on a second stream (launch_open_split; tlsgpu_set_open_parts forces
+    the form on these small batches).  "chains": the decrypt and padding pass of chain range
+    h+1 beside the MAC pass of range h -- 6,000 connections of 1-6 records of 1-700 B.
+    "blocks" (round 5): every record's tail blocks and the padding pass first, then block
+    range h+1 of every record beside the MAC of the payload ranges <= h produced, the hash
+    state carried in the workspace -- 900 connections of 1-4 records of 1 B-16 KiB, so
+    records end in every part.  ~3 % of records tampered (a bit flipped anywhere: payload,
+    MAC or padding) or truncated, connection (stop-on-alert) semantics: every status,
+    plaintext and final state equals the oracle's, across the part boundaries
+    (tlsrecordlayer.py:958-1044)."""
     from oracle import oracle as O
     from tlslite_amd import _native as N
     from tlslite_amd.device import cu_count
-    from tlslite_amd.recordlayer import open_records, set_open_parts_min_records
+    from tlslite_amd.recordlayer import open_records, set_open_parts
     T = _T()
-    rng = np.random.default_rng(zlib.crc32(repr(("parts", suite, version)).encode()))
+    rng = np.random.default_rng(zlib.crc32(repr(("parts", suite, version, mode)).encode()))
     amap = {0: 0, O.ALERT_BAD_RECORD_MAC: N.ALERT_BAD_RECORD_MAC,
             O.ALERT_DECRYPTION_FAILED: N.ALERT_DECRYPTION_FAILED}
-    nconn = 6000
+    nconn, per, maxlen = (6000, 7, 701) if mode == "chains" else (900, 5, 16385)
     writers, readers, oreaders, plan = [], [], [], []
     for ci in range(nconn):
         mk_t, mk_o = _mk(T, O, suite, version, rng)
         writers.append(mk_t())
         readers.append(mk_t())
         oreaders.append(mk_o())
-        for _ in range(int(rng.integers(1, 7))):
-            plan.append((ci, rng.bytes(int(rng.integers(1, 701))), int(rng.choice([21, 22, 23], p=[0.05, 0.05, 0.9]))))
-    assert len(plan) >= 4 * 16 * cu_count(), "too few records for a part's decrypt to fill the chip"
+        for _ in range(int(rng.integers(1, per))):
+            plan.append((ci, rng.bytes(int(rng.integers(1, maxlen))), int(rng.choice([21, 22, 23], p=[0.05, 0.05, 0.9]))))
+    if mode == "chains":
+        assert len(plan) >= 4 * 16 * cu_count(), "too few records for a part's decrypt to fill the chip"
     wires = T.seal(writers, plan)
     recs = []
     for (ci, _, ct), w in zip(plan, wires):
@@ -307,11 +315,11 @@ def test_split_open_parts_like_oracle(suite, version):
         elif u < 0.03:
             body = body[:-1]
         recs.append((ci, ct, bytes(body)))
-    set_open_parts_min_records(1)
+    set_open_parts(N.OPEN_SPLIT_CHAINS if mode == "chains" else N.OPEN_SPLIT_BLOCKS, 1)
     try:
         res = open_records(readers, recs)
     finally:
-        set_open_parts_min_records(None)
+        set_open_parts()
     stopped = set()
     for (ci, ct, body), (st, p) in zip(recs, res):
         if ci in stopped:

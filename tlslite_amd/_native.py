@@ -17,6 +17,7 @@ FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
 OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH = 0, -1, -2, -3, -4, -5
 ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED, ALERT_SKIPPED = -20, -21, -22
 CHAIN_STOP_ON_ALERT = 1
+OPEN_SPLIT_AUTO, OPEN_SPLIT_CHAINS, OPEN_SPLIT_BLOCKS, OPEN_SPLIT_NONE = 0, 1, 2, 3
 ABI_VERSION = 6
 CONN_STATE_BYTES = 2048
 
@@ -109,7 +110,7 @@ SIGNATURES = [
     ("tlsgpu_host_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32]),
     ("tlsgpu_open_workspace_bytes", _sz, [_u32]),
     ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32, _vp, _sz, _vp]),
-    ("tlsgpu_set_open_parts_min_records", _i, [ctypes.c_int64]),
+    ("tlsgpu_set_open_parts", _i, [_i, ctypes.c_int64]),
     ("tlsgpu_cipher_dev", _i, [_vp, _u32, _vp, _vp, _vp, _i, _i, _vp]),
     ("tlsgpu_derive_states_dev", _i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("tlsgpu_fill_pattern", _i, [_vp, _sz, _u64, _u64, _vp]),

@@ -60,7 +60,8 @@ hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nc
 // the split open's library-owned second streams and events (one per device and priority)
 hipError_t release_open_aux();
 size_t open_aux_count();
-void set_open_parts_min_records(long long n);
+// the open's split form and record threshold (tlsgpu_set_open_parts); -1 for a bad mode
+int set_open_parts(int mode, long long min_records);
 hipError_t launch_derive(const tlsgpu_derive_desc* descs, uint32_t n, ConnState* ws, ConnState* rs,
                          uint8_t* master_out, uint8_t* kb_out, int32_t* status, hipStream_t s);
 hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, hipStream_t s);

@@ -50,6 +50,41 @@ static_assert(sizeof(OpenMeta) == 48, "OpenMeta");
 constexpr uint32_t OM_DEC = 1, OM_VERIFY = 2, OM_PADOK = 4;
 constexpr int O3_THREADS = 1024;
 
+// The hash state of a record's MAC between the passes of an open in block-range parts
+// (launch_open_split): RecMac's h[] and its window tail prev[].
+struct OpenMacState {
+    uint32_t h[8];
+    uint32_t prev[4];
+};
+static_assert(sizeof(OpenMacState) == 48, "OpenMacState");
+
+// Ciphertext blocks [lo, hi) of a record of nb blocks that pass `part` of an open in
+// `nparts` block-range parts decrypts (round 5):
+//   part < 0        every block (an open in one pass, or in chain-range parts);
+//   part == nparts  the tail: the last 256 / BS + 1 blocks, which hold every padding byte
+//                   (tlsrecordlayer.py:979-993: up to 255 + 1 bytes), decrypted first so
+//                   that the padding pass -- and with it the MAC's length field -- is
+//                   known before the first MAC part;
+//   part h          the h-th of nparts 64-block-aligned pieces of the blocks before the tail.
+template <uint32_t BS>
+__device__ __forceinline__ void open_part_blocks(uint32_t nb, int part, int nparts, uint32_t& lo, uint32_t& hi) {
+    constexpr uint32_t TB = 256u / BS + 1u;
+    if (part < 0) {
+        lo = 0;
+        hi = nb;
+        return;
+    }
+    const uint32_t tail = nb > TB ? nb - TB : 0u;
+    if (part >= nparts) {
+        lo = tail;
+        hi = nb;
+        return;
+    }
+    const uint32_t chunks = (tail + 63u) >> 6;
+    lo = min(tail, 64u * (chunks * (uint32_t)part / (uint32_t)nparts));
+    hi = min(tail, 64u * (chunks * (uint32_t)(part + 1) / (uint32_t)nparts));
+}
+
 // LDS addressing of the equivalent-inverse-cipher tables (FIPS-197 5.3.5,
 // rijndael.py:321-362): the Td tables in the encryption tables' layout (aes_lds_fill with
 // dec = true) plus the 32-copy inverse S-box for the last round (lane_aes_dec).
@@ -181,11 +216,23 @@ __device__ __forceinline__ uint64_t open_dec_batch(const OpenMeta* meta, uint32_
     return __ballot(mine);
 }
 
+// Lane l of wave-wide value v from lane l - 1 (DPP wave_shr:1, one VALU); lane 0 gets `first`
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t first) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xf, 0xf, false);
+}
+
+// A wave walks one record (its blocks [lo, hi) of this pass, open_part_blocks) 64 blocks (one
+// 1 KiB chunk) at a time.  Round 5: the next chunk's
+// ciphertext is loaded before the current one is decrypted (its HBM latency hides under the
+// chunk's ten rounds instead of stalling the wave at every chunk), and a lane's predecessor
+// block C_{b-1} is its left neighbour's ciphertext, moved over by DPP (wave_shr:1) -- only lane
+// 0 takes it from the previous chunk's lane 63 (readlane) or the record's first predecessor
+// (OpenMeta.pred), instead of every lane loading the block again.
 template <int NR>
 __global__ void __launch_bounds__(O3_THREADS, 1)
 open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
                 uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
-                uint32_t epoch, uint32_t c_lo, uint32_t c_hi) {
+                uint32_t epoch, uint32_t c_lo, uint32_t c_hi, int part, int nparts) {
     aes_lds_fill(nullptr, true);
     __syncthreads();
     QuadAesDec D;
@@ -204,19 +251,32 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
         const uint8_t* C = wire + R.ct_off;
         uint8_t* P = pt + R.pt_off;
         const uint32_t* dk = st->dk;  // wave-uniform: scalar loads (in VGPRs measured 3 % slower)
-        for (uint32_t b = lane; b < nb; b += 64) {
-            uint32_t c[4], p[4];
-            load16(C + 16 * b, c);
-            if (b == 0) {
+        uint32_t lo, hi;
+        open_part_blocks<16>(nb, part, nparts, lo, hi);
+        if (lo >= hi) continue;
+        uint32_t carry[4] = {mt.pred[0], mt.pred[1], mt.pred[2], mt.pred[3]};
+        if (lo) load16(C + 16 * (lo - 1), carry);  // wave-uniform: the block before this pass's first
+        uint32_t c[4] = {0, 0, 0, 0};
+        if (lo + lane < hi) load16(C + 16 * (lo + lane), c);
+        for (uint32_t base = lo; base < hi; base += 64) {
+            const uint32_t b = base + lane;
+            uint32_t cn[4] = {0, 0, 0, 0};
+            if (b + 64 < hi) load16(C + 16 * (b + 64), cn);  // the next chunk, in flight meanwhile
+            uint32_t p[4];
 #pragma unroll
-                for (int i = 0; i < 4; i++) p[i] = mt.pred[i];
-            } else {
-                load16(C + 16 * (b - 1), p);
+            for (int i = 0; i < 4; i++) {
+                p[i] = wave_shr1(c[i], carry[i]);
+                carry[i] = __builtin_amdgcn_readlane(c[i], 63);  // the next chunk's lane-0 predecessor
             }
-            lane_aes_dec<NR>(D, c, dk);
+            if (b < hi) {
+                uint32_t d[4] = {c[0], c[1], c[2], c[3]};
+                lane_aes_dec<NR>(D, d, dk);
 #pragma unroll
-            for (int i = 0; i < 4; i++) c[i] ^= p[i];
-            if (16 * b >= E) store16(P + 16 * b - E, c);
+                for (int i = 0; i < 4; i++) d[i] ^= p[i];
+                if (16 * b >= E) store16(P + 16 * b - E, d);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) c[i] = cn[i];
         }
     }
 }
@@ -281,7 +341,7 @@ struct DesLane {
 __global__ void __launch_bounds__(OT_THREADS, 1)
 open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
                  uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
-                 uint32_t epoch, uint32_t c_lo, uint32_t c_hi) {
+                 uint32_t epoch, uint32_t c_lo, uint32_t c_hi, int part, int nparts) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ot_lds[];
     des_lds_fill(ot_lds);  // the kernel's only LDS: the tables start at LDS byte 0
     __syncthreads();
@@ -301,19 +361,32 @@ open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
         const uint32_t nb = R.ct_len >> 3;
         const uint8_t* C = wire + R.ct_off;
         uint8_t* P = pt + R.pt_off;
-        for (uint32_t b = lane; b < nb; b += 64) {
-            uint32_t c[2], p[2];
-            load8(C + 8 * b, c);
-            if (b == 0) {
-                p[0] = mt.pred[0];
-                p[1] = mt.pred[1];
-            } else {
-                load8(C + 8 * (b - 1), p);
+        // next chunk prefetched, predecessor from the left neighbour (as open_aes_kernel)
+        uint32_t lo, hi;
+        open_part_blocks<8>(nb, part, nparts, lo, hi);
+        if (lo >= hi) continue;
+        uint32_t carry[2] = {mt.pred[0], mt.pred[1]};
+        if (lo) load8(C + 8 * (lo - 1), carry);
+        uint32_t c[2] = {0, 0};
+        if (lo + lane < hi) load8(C + 8 * (lo + lane), c);
+        for (uint32_t base = lo; base < hi; base += 64) {
+            const uint32_t b = base + lane;
+            uint32_t cn[2] = {0, 0};
+            if (b + 64 < hi) load8(C + 8 * (b + 64), cn);
+            uint32_t p[2];
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                p[i] = wave_shr1(c[i], carry[i]);
+                carry[i] = __builtin_amdgcn_readlane(c[i], 63);
             }
-            uint32_t hi = bswap32(c[0]), lo = bswap32(c[1]);
-            L.decrypt(hi, lo, ks);
-            uint32_t d[2] = {bswap32(hi) ^ p[0], bswap32(lo) ^ p[1]};
-            if (8 * b >= E) store8(P + 8 * b - E, d);
+            if (b < hi) {
+                uint32_t whi = bswap32(c[0]), wlo = bswap32(c[1]);
+                L.decrypt(whi, wlo, ks);
+                uint32_t d[2] = {bswap32(whi) ^ p[0], bswap32(wlo) ^ p[1]};
+                if (8 * b >= E) store8(P + 8 * b - E, d);
+            }
+            c[0] = cn[0];
+            c[1] = cn[1];
         }
     }
 }
@@ -373,13 +446,26 @@ __global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __res
 // round 4: cfg2 718 vs 733, cfg3 397 vs 402 GiB/s -- with one lane per 16 KiB record the
 // open's MAC is latency-bound, and the transposes sit on that path;
 // profiles/r04/ab/ab_open_r04.txt.)
-template <int MAC, bool SSL3>
+// part < 0: the whole MAC in one pass.  Block-range parts (round 5): pass h < nparts hashes
+// the payload chunks whose blocks the decrypt parts 0..h (and the tail) have produced and
+// keeps the hash state in the workspace (OpenMacState); pass nparts hashes the rest,
+// finishes and compares.
+template <int BS>
+__device__ __forceinline__ uint32_t open_chunks_ready(uint32_t nb, uint32_t E, uint32_t nfull, int part, int nparts) {
+    uint32_t lo, hi;
+    open_part_blocks<BS>(nb, part, nparts, lo, hi);
+    const uint32_t bytes = BS * hi > E ? BS * hi - E : 0u;  // payload bytes decrypted from its start
+    return min(nfull, bytes >> 6);
+}
+
+template <int MAC, bool SSL3, int BS>
 __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
                                                       const uint8_t* __restrict__ pt,
                                                       const ConnState* __restrict__ states,
                                                       int32_t* __restrict__ status,
-                                                      const OpenMeta* __restrict__ meta, uint32_t epoch,
-                                                      uint32_t c_lo, uint32_t c_hi) {
+                                                      const OpenMeta* __restrict__ meta, OpenMacState* __restrict__ ms,
+                                                      uint32_t epoch, uint32_t c_lo, uint32_t c_hi, int part,
+                                                      int nparts) {
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -391,11 +477,35 @@ __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record*
     const tlsgpu_open_record R = recs[r];
     const uint8_t* P = pt + R.pt_off;
     const uint32_t n = mt.n;
-    M mac;
-    mac.begin(st, mt.seq, R.content_type, n);
     const uint32_t nfull = n >> 6;
-    if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, P, nfull);
-    else mac_bulk<false>(mac, P, nfull);
+    M mac;
+    uint32_t c0 = 0, c1 = nfull;
+    if (part >= 0) {
+        const uint32_t E = st->explicit_iv ? (uint32_t)BS : 0u;
+        const uint32_t nb = R.ct_len / BS;
+        c0 = part == 0 ? 0u : open_chunks_ready<BS>(nb, E, nfull, part - 1, nparts);
+        c1 = part == nparts ? nfull : open_chunks_ready<BS>(nb, E, nfull, part, nparts);
+    }
+    if (c0 == 0) {
+        mac.begin(st, mt.seq, R.content_type, n);
+    } else {
+        const OpenMacState& q = ms[r];
+#pragma unroll
+        for (int k = 0; k < 8; k++) mac.h[k] = q.h[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) mac.prev[k] = q.prev[k];
+    }
+    const uint8_t* Pc = P + 64 * c0;
+    if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, Pc, c1 - c0);
+    else mac_bulk<false>(mac, Pc, c1 - c0);
+    if (part >= 0 && part < nparts) {  // more parts follow: keep the hash state
+        OpenMacState& q = ms[r];
+#pragma unroll
+        for (int k = 0; k < 8; k++) q.h[k] = mac.h[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) q.prev[k] = mac.prev[k];
+        return;
+    }
     uint32_t tail[16];
     load_partial(P + 64 * nfull, n & 63, tail);
     uint32_t m[8];

@@ -347,10 +347,11 @@ def open_dev(chains, nchains, records, nrecords, wire, pt, states, status, varia
            stream.handle if stream is not None else None)
 
 
-def set_open_parts_min_records(n):
-    """Record count from which an open runs in parts (None / negative: the library default);
-    tests lower it to exercise the parts path on small batches."""
-    N.call("tlsgpu_set_open_parts_min_records", -1 if n is None else int(n))
+def set_open_parts(mode=N.OPEN_SPLIT_AUTO, min_records=0):
+    """How CBC-suite opens are split (process-wide): N.OPEN_SPLIT_AUTO (the library picks),
+    N.OPEN_SPLIT_CHAINS / N.OPEN_SPLIT_BLOCKS (that form for every batch of >= min_records
+    records: tests run each form on small batches), N.OPEN_SPLIT_NONE (one pass each)."""
+    N.call("tlsgpu_set_open_parts", int(mode), int(min_records))
 
 
 def open_records(states, records, stream=None, stop_on_alert=True):

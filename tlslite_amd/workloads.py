@@ -76,8 +76,9 @@ class Workload:
         order = np.arange(r) if rec_order is None else np.asarray(rec_order)
         self.slot_of = np.empty(r, dtype=np.int64)
         self.slot_of[order] = np.arange(r)
-        # plaintext slots at pt_align-byte boundaries (16: packed; bench.py uses 128 so every record
-        # starts on a line: the MAC kernel's 64-B chunks then never straddle two lines)
+        # plaintext slots at pt_align-byte boundaries (16: packed, bench.py's default since round 4,
+        # as a TLS stack fills an arena; bench.py --pt-align 128 puts every record on a line, so the
+        # MAC kernel's 64-B chunks never straddle two -- round 3's cfg3 figures used that layout)
         self.pt_align = int(pt_align)
         pt_stride = np.array([_round_up(int(x), self.pt_align) for x in self.pt_len])
         wlen = np.array([self._wire_len(g, int(n)) for g, n in self._rec_groups()], dtype=np.int64)

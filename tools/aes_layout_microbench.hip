@@ -14,6 +14,12 @@
 //   mixN    (argv[2] = "m") 32 N chains on N pair waves, the rest on quad waves (N = 4: half and
 //           half, 12 waves/CU)
 //   *@512   the same at 512 chains per CU (cfg3 has 4,096 per CU)
+//   trace mode (argv[2] = "t", round 5): the product pair round at 256 chains per CU, every
+//   wave time-stamping (s_memtime) the start of NS consecutive blocks; the host derives each
+//   wave's round period and the phase of every same-CU wave pair within a round (do the 8
+//   waves convoy -- issue their rounds together -- or spread?), with and without a
+//   mac_kernel-shaped SHA-1 co-runner, and for start-staggered variants (waves delayed by
+//   w/8 or (w&1)/2 of a round before the loop)
 //   latency mode (argv[2] = "lat"): 2 and 16 chains per CU (cfg4 at 8 GPUs / 1 GPU):
 //   the round is then one chain's dependent latency, reported in shader cycles;
 //   quad1s = quad1b with ONE chain per wave (chains spread over the SIMDs)
@@ -276,6 +282,59 @@ __global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict_
     }
 }
 
+// Trace kernel (mode "t"): the pair layout of bench_kernel (LAYOUT 2, 256 chains per CU)
+// with per-wave block-start time stamps.  STAGGER 0: no delay; 1: wave w waits w/8 of a
+// round before its loop; 2: odd waves wait half a round.  round_cyc: the delay unit.
+constexpr int TR_NS = 64;     // time-stamped blocks per wave
+constexpr int TR_B0 = 200;    // first time-stamped block (the waves have settled by then)
+template <int STAGGER>
+__global__ void __launch_bounds__(512) trace_kernel(const uint32_t* __restrict__ ek, uint32_t* __restrict__ out,
+                                                    uint64_t* __restrict__ trace, int blocks, int round_cyc) {
+    aes_lds_fill(nullptr, false);
+    __syncthreads();
+    __builtin_amdgcn_s_setprio(1);
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    PairAes P;
+    P.init();
+    const uint32_t h = lane & 1;
+    const uint32_t ch = blockIdx.x * 256 + wave * 32 + (lane >> 1);
+    const uint32_t ca = 2 * h, pa = 2 * (1 - h);
+    const uint32_t kwa = ek[ca], kwb = ek[ca + 1];
+    uint32_t ka[NR + 1], kb[NR + 1];
+#pragma unroll
+    for (int r = 1; r <= NR; r++) {
+        ka[r] = ek[4 * r + pa];
+        kb[r] = ek[4 * r + pa + 1];
+    }
+    uint32_t a = init_word(ch, ca), bb = init_word(ch, ca + 1);
+    if (STAGGER) {
+        const uint64_t d = STAGGER == 1 ? (uint64_t)round_cyc * wave / 8 : (wave & 1) ? (uint64_t)round_cyc / 2 : 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < d) {
+        }
+    }
+    uint64_t* tr = trace + ((size_t)blockIdx.x * 8 + wave) * (TR_NS + 2);
+    const uint64_t tl0 = __builtin_amdgcn_s_memtime();
+    for (int b = 0; b < blocks; b++) {
+        if (b >= TR_B0 && b < TR_B0 + TR_NS) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            if (lane == 0) tr[b - TR_B0] = t;
+        }
+        a ^= kwa;
+        bb ^= kwb;
+#pragma unroll
+        for (int r = 1; r < NR; r++) P.round(a, bb, ka[r], kb[r]);
+        P.last(a, bb, ka[NR], kb[NR]);
+    }
+    const uint64_t tl1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+        tr[TR_NS] = tl0;
+        tr[TR_NS + 1] = tl1;
+    }
+    out[ch * 4 + ca] = a;
+    out[ch * 4 + ca + 1] = bb;
+}
+
 // VALU co-runner shaped like mac_kernel: one lane per "record", SHA-1 compressions
 // on register data, one 256-thread block per CU (one wave per SIMD).
 __global__ void __launch_bounds__(256) sha_corun(uint32_t* out, int iters) {
@@ -363,6 +422,87 @@ static int compare(const std::vector<Res>& rs) {
     return bad;
 }
 
+// mode "t": run trace_kernel<STAGGER> (+ optional co-runner), print per-wave round periods and
+// the same-CU pair phase histogram
+template <int STAGGER>
+static std::vector<uint32_t> trace_run(const char* name, const uint32_t* d_ek, int cus, int blocks, int corun,
+                                       int round_cyc) {
+    auto kern = trace_kernel<STAGGER>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              AES_LDS_BYTES);
+    uint32_t* d_out;
+    uint64_t* d_tr;
+    const size_t ntr = (size_t)cus * 8 * (TR_NS + 2);
+    (void)hipMalloc(&d_out, (size_t)cus * 256 * 16);
+    (void)hipMalloc(&d_tr, ntr * 8);
+    hipLaunchKernelGGL(kern, dim3(cus), dim3(512), AES_LDS_BYTES, 0, d_ek, d_out, d_tr, TR_B0 + TR_NS + 8, round_cyc);
+    (void)hipDeviceSynchronize();
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    if (corun) hipLaunchKernelGGL(sha_corun, dim3(cus), dim3(256), 0, g_side, g_side_out, corun);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(kern, dim3(cus), dim3(512), AES_LDS_BYTES, 0, d_ek, d_out, d_tr, blocks, round_cyc);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    (void)hipDeviceSynchronize();
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    std::vector<uint64_t> tr(ntr);
+    (void)hipMemcpy(tr.data(), d_tr, ntr * 8, hipMemcpyDeviceToHost);
+    std::vector<uint32_t> out((size_t)cus * 256 * 4);
+    (void)hipMemcpy(out.data(), d_out, out.size() * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_tr);
+    // per wave: round period over the stamped blocks; loop cycles per round
+    double per_sum = 0, loop_sum = 0;
+    int hist[10] = {0};
+    int npairs = 0;
+    double spread_sum = 0;  // per CU and block: max - min block-start over the 8 waves, in rounds
+    int nspread = 0;
+    for (int c = 0; c < cus; c++) {
+        double per[8];
+        for (int w = 0; w < 8; w++) {
+            const uint64_t* t = &tr[((size_t)c * 8 + w) * (TR_NS + 2)];
+            per[w] = (double)(t[TR_NS - 1] - t[0]) / ((TR_NS - 1) * NR);
+            per_sum += per[w];
+            loop_sum += (double)(t[TR_NS + 1] - t[TR_NS]) / ((double)blocks * NR);
+        }
+        for (int b = 0; b < TR_NS; b++) {
+            uint64_t lo = ~0ull, hi = 0;
+            for (int w = 0; w < 8; w++) {
+                const uint64_t x = tr[((size_t)c * 8 + w) * (TR_NS + 2) + b];
+                lo = x < lo ? x : lo;
+                hi = x > hi ? x : hi;
+            }
+            spread_sum += (double)(hi - lo) / per[0];
+            nspread++;
+        }
+        // phase of wave w' relative to wave w within a round, sampled at every stamped block
+        for (int w = 0; w < 8; w++)
+            for (int v = w + 1; v < 8; v++)
+                for (int b = 0; b < TR_NS; b += 4) {
+                    const double P = 0.5 * (per[w] + per[v]);
+                    const double d = (double)(int64_t)(tr[((size_t)c * 8 + v) * (TR_NS + 2) + b] -
+                                                       tr[((size_t)c * 8 + w) * (TR_NS + 2) + b]);
+                    double f = d / P - __builtin_floor(d / P);
+                    int k = (int)(f * 10.0);
+                    k = k < 0 ? 0 : (k > 9 ? 9 : k);
+                    hist[k]++;
+                    npairs++;
+                }
+    }
+    const double nw = cus * 8.0;
+    printf("%-10s%s  %7.3f ms (cfg2-equiv %.3f)  round period %6.1f cyc (stamped blocks), loop %6.1f cyc/round  "
+           "block-start spread over the CU's 8 waves %.2f rounds\n  pair phase within a round (10 bins, %% of %d):",
+           name, corun ? " +sha" : "     ", ms, ms * 1027.0 / blocks, per_sum / nw, loop_sum / nw, spread_sum / nspread,
+           npairs);
+    for (int k = 0; k < 10; k++) printf(" %4.1f", 100.0 * hist[k] / npairs);
+    printf("\n");
+    fflush(stdout);
+    return out;
+}
+
 int main(int argc, char** argv) {
     const int blocks = argc > 1 ? atoi(argv[1]) : 1027;
     int dev = 0, cus = 0;
@@ -376,6 +516,20 @@ int main(int argc, char** argv) {
     (void)hipMemcpy(d_ek, ek, sizeof(ek), hipMemcpyHostToDevice);
     (void)hipStreamCreateWithFlags(&g_side, hipStreamNonBlocking);
     (void)hipMalloc(&g_side_out, (size_t)cus * 256 * 4);
+    if (argc > 2 && argv[2][0] == 't') {  // trace: do the pair waves convoy?
+        std::vector<std::vector<uint32_t>> o;
+        const int rc = 192;  // the measured round period (cycles) the stagger variants delay by
+        o.push_back(trace_run<0>("pair1", d_ek, cus, blocks, 0, rc));
+        o.push_back(trace_run<1>("pair1-st8", d_ek, cus, blocks, 0, rc));
+        o.push_back(trace_run<2>("pair1-st2", d_ek, cus, blocks, 0, rc));
+        o.push_back(trace_run<0>("pair1", d_ek, cus, blocks, 2 * blocks, rc));
+        o.push_back(trace_run<1>("pair1-st8", d_ek, cus, blocks, 2 * blocks, rc));
+        o.push_back(trace_run<2>("pair1-st2", d_ek, cus, blocks, 2 * blocks, rc));
+        int bad = 0;
+        for (size_t i = 1; i < o.size(); i++) bad |= o[i] != o[0];
+        printf(bad ? "MISMATCH between trace variants\n" : "all trace variants agree\n");
+        return bad;
+    }
     if (argc > 2 && argv[2][0] == 'l') {  // latency regime (cfg4)
         std::vector<Res> l2, l16;
         l2.push_back(run<4, 1, 2>("quad1", d_ek, cus, blocks));
