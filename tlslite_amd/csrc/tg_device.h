@@ -124,8 +124,11 @@ __device__ __forceinline__ void aes_lds_fill(uint32_t* lds, bool dec) {
         for (uint32_t idx = threadIdx.x; idx < 8192; idx += blockDim.x) {
             uint32_t e = idx >> 5, c = idx & 31;
             uint32_t byte = 131072 + e * 128 + c * 4;
-            if (lds) lds[byte >> 2] = c_aes.inv_sbox[e];
-            else *(l3_t*)(size_t)byte = c_aes.inv_sbox[e];
+            // the byte in all four byte lanes: the open path's last round picks each output
+            // byte straight out of its lookup with v_perm (tg_open3.h lane_aes_dec)
+            const uint32_t v = (uint32_t)c_aes.inv_sbox[e] * 0x01010101u;
+            if (lds) lds[byte >> 2] = v;
+            else *(l3_t*)(size_t)byte = v;
         }
     }
 }
@@ -149,7 +152,7 @@ struct AesLds {
     template <int B>
     __device__ __forceinline__ uint32_t isb(uint32_t s) const {
         uint32_t idx = (s >> (8 * B)) & 0xff;
-        return *(const uint32_t*)(base + 131072 + idx * 128 + lo);
+        return *(const uint32_t*)(base + 131072 + idx * 128 + lo) & 0xffu;  // entries replicate the byte
     }
 };
 

@@ -89,16 +89,23 @@ __device__ __forceinline__ void open_part_blocks(uint32_t nb, int part, int npar
 // rijndael.py:321-362): the Td tables in the encryption tables' layout (aes_lds_fill with
 // dec = true) plus the 32-copy inverse S-box for the last round (lane_aes_dec).
 struct QuadAesDec {
-    QuadAes t;  // same LDS addressing as the encryption tables (decrypt fill)
-    uint32_t isb_base;
+    QuadAes t;     // same LDS addressing as the encryption tables (decrypt fill)
+    uint32_t isw;  // inverse S-box address word: byte 0 = copy * 8, byte 2 = 0x04 (see isb)
     __device__ __forceinline__ void init() {
         t.init();
-        isb_base = 131072u + (__lane_id() & 31) * 4;
+        isw = ((__lane_id() & 31) * 8u) | 0x40000u;  // lane-dependent: a VGPR
     }
+    // InvS[byte B of x], replicated in all four bytes (aes_lds_fill): the entry of byte value
+    // e, copy c sits at 0x20000 + e * 128 + c * 4 = (perm(x -> byte 1, isw) >> 1) -- one v_perm
+    // and one 2-cycle shift per lookup (round 4: bfe + shift-or + a shift of the result)
     template <int B>
-    __device__ __forceinline__ uint32_t isb(uint32_t x) const {  // InvS[byte B of x] << 8B
-        const uint32_t idx = __builtin_amdgcn_ubfe(x, 8 * B, 8);
-        return lds_read32(idx * 128u + isb_base) << (8 * B);
+    __device__ __forceinline__ uint32_t isb(uint32_t x) const {
+        constexpr uint32_t sel = 0x0c000000u | (2u << 16) | ((4u + B) << 8) | 0u;
+        return lds_read32(perm(x, isw, sel) >> 1);
+    }
+    // bytes 0..3 of the output column from four replicated lookups (two v_perm), key XOR-ed
+    __device__ __forceinline__ static uint32_t col(uint32_t r0, uint32_t r1, uint32_t r2, uint32_t r3, uint32_t k) {
+        return __builtin_amdgcn_bitop3_b32(perm(r1, r0, 0x0c0c0500u), perm(r3, r2, 0x07020c0cu), k, 0x96);
     }
 };
 
@@ -196,10 +203,10 @@ __device__ __forceinline__ void lane_aes_dec(const QuadAesDec& D, uint32_t s[4],
         s0 = t0; s1 = t1; s2 = t2; s3 = t3;
     }
     const uint32_t* k = dk + 4 * NR;
-    s[0] = (D.isb<0>(s0) | D.isb<1>(s3) | D.isb<2>(s2) | D.isb<3>(s1)) ^ k[0];
-    s[1] = (D.isb<0>(s1) | D.isb<1>(s0) | D.isb<2>(s3) | D.isb<3>(s2)) ^ k[1];
-    s[2] = (D.isb<0>(s2) | D.isb<1>(s1) | D.isb<2>(s0) | D.isb<3>(s3)) ^ k[2];
-    s[3] = (D.isb<0>(s3) | D.isb<1>(s2) | D.isb<2>(s1) | D.isb<3>(s0)) ^ k[3];
+    s[0] = QuadAesDec::col(D.isb<0>(s0), D.isb<1>(s3), D.isb<2>(s2), D.isb<3>(s1), k[0]);
+    s[1] = QuadAesDec::col(D.isb<0>(s1), D.isb<1>(s0), D.isb<2>(s3), D.isb<3>(s2), k[1]);
+    s[2] = QuadAesDec::col(D.isb<0>(s2), D.isb<1>(s1), D.isb<2>(s0), D.isb<3>(s3), k[2]);
+    s[3] = QuadAesDec::col(D.isb<0>(s3), D.isb<1>(s2), D.isb<2>(s1), D.isb<3>(s0), k[3]);
 }
 
 // The records a decrypt wave handles: r0 + i * nwaves for i < 64 (the wave's next 64,
@@ -221,13 +228,54 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t first) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// The records a decrypt wave opens, one after another (open_dec_batch's batches of 64
+// candidates, those of this launch's part), with the NEXT record's descriptor and round keys
+// loaded while the current one is decrypted (round 5): lane i holds word i of the next
+// record's OpenMeta (0..11) and tlsgpu_open_record (12..17) in `vm`, word i of its state's
+// equivalent-inverse round keys (0..4 NR + 3) and the explicit-IV flag (lane 63) in `vk`;
+// at the switch they become wave-uniform (v_readlane).  Before, each record began with three
+// dependent scalar loads (meta -> state -> round keys, ~1 us each) in front of its first
+// chunk, 17 chunks of work apart on cfg2 and 5 passes apart in block-range parts.
+struct OpenDecStream {
+    const OpenMeta* meta;
+    uint32_t nrecords, nwaves, epoch, c_lo, c_hi;
+    uint32_t r0;
+    uint64_t mask;
+    __device__ __forceinline__ uint32_t next() {  // the next record of the wave, or ~0u
+        while (!mask) {
+            r0 += 64 * nwaves;
+            if (r0 >= nrecords) return ~0u;
+            mask = open_dec_batch(meta, nrecords, r0, nwaves, epoch, c_lo, c_hi);
+        }
+        const uint32_t r = r0 + (uint32_t)__builtin_ctzll(mask) * nwaves;
+        mask &= mask - 1;
+        return r;
+    }
+};
+__device__ __forceinline__ uint32_t open_fetch_desc(const OpenMeta* meta, const tlsgpu_open_record* recs, uint32_t r) {
+    const uint32_t lane = __lane_id();
+    if (r == ~0u) return 0u;
+    if (lane < 12) return ((const uint32_t*)(meta + r))[lane];
+    if (lane < 18) return ((const uint32_t*)(recs + r))[lane - 12];
+    return 0u;
+}
+template <int NR>
+__device__ __forceinline__ uint32_t open_fetch_keys(const ConnState* states, uint32_t vm, uint32_t r) {
+    const uint32_t lane = __lane_id();
+    if (r == ~0u) return 0u;
+    const ConnState* st = states + __builtin_amdgcn_readlane(vm, 6);  // OpenMeta.state
+    if (lane < 4 * (NR + 1)) return st->dk[lane];
+    if (lane == 63) return st->explicit_iv;
+    return 0u;
+}
+
 // A wave walks one record (its blocks [lo, hi) of this pass, open_part_blocks) 64 blocks (one
-// 1 KiB chunk) at a time.  Round 5: the next chunk's
-// ciphertext is loaded before the current one is decrypted (its HBM latency hides under the
-// chunk's ten rounds instead of stalling the wave at every chunk), and a lane's predecessor
-// block C_{b-1} is its left neighbour's ciphertext, moved over by DPP (wave_shr:1) -- only lane
-// 0 takes it from the previous chunk's lane 63 (readlane) or the record's first predecessor
-// (OpenMeta.pred), instead of every lane loading the block again.
+// 1 KiB chunk) at a time.  Round 5: the next chunk's ciphertext is loaded before the current
+// one is decrypted (its HBM latency hides under the chunk's ten rounds instead of stalling the
+// wave at every chunk), and a lane's predecessor block C_{b-1} is its left neighbour's
+// ciphertext, moved over by DPP (wave_shr:1) -- only lane 0 takes it from the previous
+// chunk's lane 63 (readlane) or the record's first predecessor (OpenMeta.pred), instead of
+// every lane loading the block again.
 template <int NR>
 __global__ void __launch_bounds__(O3_THREADS, 1)
 open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
@@ -239,45 +287,72 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
     D.init();
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t nwaves = gridDim.x * (O3_THREADS / 64);
-    for (uint32_t r0 = blockIdx.x * (O3_THREADS / 64) + wv; r0 < nrecords; r0 += 64 * nwaves)
-    for (uint64_t mask = open_dec_batch(meta, nrecords, r0, nwaves, epoch, c_lo, c_hi); mask; mask &= mask - 1) {
-        const uint32_t r = r0 + (uint32_t)__builtin_ctzll(mask) * nwaves;
-        const OpenMeta& mt = meta[r];
-        const ConnState* st = states + mt.state;
-        const tlsgpu_open_record R = recs[r];
-        const uint32_t E = st->explicit_iv ? 16u : 0u;
-        const uint32_t nb = R.ct_len >> 4;
-        const uint8_t* C = wire + R.ct_off;
-        uint8_t* P = pt + R.pt_off;
-        const uint32_t* dk = st->dk;  // wave-uniform: scalar loads (in VGPRs measured 3 % slower)
+    OpenDecStream rs;
+    rs.meta = meta;
+    rs.nrecords = nrecords;
+    rs.nwaves = gridDim.x * (O3_THREADS / 64);
+    rs.epoch = epoch;
+    rs.c_lo = c_lo;
+    rs.c_hi = c_hi;
+    rs.r0 = blockIdx.x * (O3_THREADS / 64) + wv;
+    rs.mask = rs.r0 < nrecords ? open_dec_batch(meta, nrecords, rs.r0, rs.nwaves, epoch, c_lo, c_hi) : 0ull;
+    uint32_t r = rs.next();
+    uint32_t vm = open_fetch_desc(meta, recs, r);
+    uint32_t vk = open_fetch_keys<NR>(states, vm, r);
+    while (r != ~0u) {
+        // this record's descriptor and keys, wave-uniform
+        uint32_t dk[4 * (NR + 1)];
+#pragma unroll
+        for (int i = 0; i < 4 * (NR + 1); i++) dk[i] = __builtin_amdgcn_readlane(vk, i);
+        const uint32_t E = __builtin_amdgcn_readlane(vk, 63) ? 16u : 0u;
+        uint32_t carry[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) carry[i] = __builtin_amdgcn_readlane(vm, i);  // OpenMeta.pred
+        const uint64_t ct_off = (uint64_t)__builtin_amdgcn_readlane(vm, 12) |
+                                ((uint64_t)__builtin_amdgcn_readlane(vm, 13) << 32);
+        const uint64_t pt_off = (uint64_t)__builtin_amdgcn_readlane(vm, 14) |
+                                ((uint64_t)__builtin_amdgcn_readlane(vm, 15) << 32);
+        const uint32_t ct_len = __builtin_amdgcn_readlane(vm, 16);
+        // the next record's descriptor now; its keys after this record's first chunk
+        const uint32_t rn = rs.next();
+        vm = open_fetch_desc(meta, recs, rn);
+        bool keys_pending = true;
+        const uint32_t nb = ct_len >> 4;
+        const uint8_t* C = wire + ct_off;
+        uint8_t* P = pt + pt_off;
         uint32_t lo, hi;
         open_part_blocks<16>(nb, part, nparts, lo, hi);
-        if (lo >= hi) continue;
-        uint32_t carry[4] = {mt.pred[0], mt.pred[1], mt.pred[2], mt.pred[3]};
-        if (lo) load16(C + 16 * (lo - 1), carry);  // wave-uniform: the block before this pass's first
-        uint32_t c[4] = {0, 0, 0, 0};
-        if (lo + lane < hi) load16(C + 16 * (lo + lane), c);
-        for (uint32_t base = lo; base < hi; base += 64) {
-            const uint32_t b = base + lane;
-            uint32_t cn[4] = {0, 0, 0, 0};
-            if (b + 64 < hi) load16(C + 16 * (b + 64), cn);  // the next chunk, in flight meanwhile
-            uint32_t p[4];
+        if (lo < hi) {
+            if (lo) load16(C + 16 * (lo - 1), carry);  // wave-uniform: the block before this pass's first
+            uint32_t c[4] = {0, 0, 0, 0};
+            if (lo + lane < hi) load16(C + 16 * (lo + lane), c);
+            for (uint32_t base = lo; base < hi; base += 64) {
+                const uint32_t b = base + lane;
+                uint32_t cn[4] = {0, 0, 0, 0};
+                if (b + 64 < hi) load16(C + 16 * (b + 64), cn);  // the next chunk, in flight meanwhile
+                uint32_t p[4];
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
-                p[i] = wave_shr1(c[i], carry[i]);
-                carry[i] = __builtin_amdgcn_readlane(c[i], 63);  // the next chunk's lane-0 predecessor
+                for (int i = 0; i < 4; i++) {
+                    p[i] = wave_shr1(c[i], carry[i]);
+                    carry[i] = __builtin_amdgcn_readlane(c[i], 63);  // the next chunk's lane-0 predecessor
+                }
+                if (b < hi) {
+                    uint32_t d[4] = {c[0], c[1], c[2], c[3]};
+                    lane_aes_dec<NR>(D, d, dk);
+#pragma unroll
+                    for (int i = 0; i < 4; i++) d[i] ^= p[i];
+                    if (16 * b >= E) store16(P + 16 * b - E, d);
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) c[i] = cn[i];
+                if (keys_pending) {
+                    vk = open_fetch_keys<NR>(states, vm, rn);
+                    keys_pending = false;
+                }
             }
-            if (b < hi) {
-                uint32_t d[4] = {c[0], c[1], c[2], c[3]};
-                lane_aes_dec<NR>(D, d, dk);
-#pragma unroll
-                for (int i = 0; i < 4; i++) d[i] ^= p[i];
-                if (16 * b >= E) store16(P + 16 * b - E, d);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; i++) c[i] = cn[i];
         }
+        if (keys_pending) vk = open_fetch_keys<NR>(states, vm, rn);
+        r = rn;
     }
 }
 

@@ -1,0 +1,139 @@
+// aes_dec_microbench.hip -- the open path's AES decrypt round loop (one lane per block,
+// lane_aes_dec of tg_open3.h: 16 Td lookups per round in the lane, 32-copy LDS tables) with
+// no global-memory traffic, to find what bounds open_aes_kernel (0.96 ms on cfg2 against a
+// 0.62 ms LDS-array floor, lds_busy 0.55 in PMC).  Variants:
+//   ILP   independent blocks per lane (1: the product; 2: two blocks' rounds interleaved)
+//   KEYV  round keys in VGPRs (1) or wave-uniform SGPRs (0: the product)
+//   W     waves per CU (16: the product's 1024-thread workgroup; 8)
+// Every variant decrypts the same blocks with the same keys; the host checks that the
+// outputs agree and prints cycles per block-round per CU, the LDS-array busy fraction it
+// implies (160 lookups per block, 32 per cycle) and the cfg2-equivalent time
+// (67.3 M blocks).  Diagnostic tool only.
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Itlslite_amd/csrc tools/aes_dec_microbench.hip -o tools/aes_dec_mb.bin
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <vector>
+#include "../tlslite_amd/csrc/tg_open3.h"
+
+using namespace tg;
+constexpr int NR = 10;
+
+template <int ILP, int KEYV, int W>
+__global__ void __launch_bounds__(64 * W, 1) dec_kernel(const uint32_t* __restrict__ dk_g, uint32_t* __restrict__ out,
+                                                       uint64_t* __restrict__ cyc, int iters) {
+    aes_lds_fill(nullptr, true);
+    __syncthreads();
+    QuadAesDec D;
+    D.init();
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t dk[4 * (NR + 1)];
+    const uint32_t* dkp = dk_g;
+    if constexpr (KEYV) {
+#pragma unroll
+        for (int i = 0; i < 4 * (NR + 1); i++) {
+            dk[i] = dk_g[i];
+            asm volatile("" : "+v"(dk[i]));  // keep the keys in VGPRs
+        }
+        dkp = dk;
+    }
+    uint32_t s[ILP][4];
+#pragma unroll
+    for (int i = 0; i < ILP; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) s[i][j] = (gid * ILP + i) * 0x9e3779b9u ^ (j * 0x85ebca6bu);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int i = 0; i < ILP; i++) lane_aes_dec<NR>(D, s[i], dkp);
+    }
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int i = 0; i < ILP; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) out[(gid * ILP + i) * 4 + j] = s[i][j];
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+struct R {
+    std::vector<uint32_t> out;
+};
+
+template <int ILP, int KEYV, int W>
+static R run(const char* name, const uint32_t* d_dk, int cus, int iters_total, int lanes_per_cu) {
+    auto kern = dec_kernel<ILP, KEYV, W>;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              AES_DEC_LDS_BYTES);
+    // the same blocks in every variant: lanes_per_cu * iters_total blocks per CU, spread as
+    // (64 W lanes x ILP) x iters
+    const int iters = iters_total * lanes_per_cu / (64 * W * ILP);
+    const size_t nout = (size_t)cus * 64 * W * ILP * 4;
+    uint32_t* d_out;
+    uint64_t* d_cyc;
+    (void)hipMalloc(&d_out, nout * 4);
+    (void)hipMalloc(&d_cyc, cus * 8);
+    hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * W), AES_DEC_LDS_BYTES, 0, d_dk, d_out, d_cyc, 4);
+    (void)hipDeviceSynchronize();
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * W), AES_DEC_LDS_BYTES, 0, d_dk, d_out, d_cyc, iters);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    std::vector<uint64_t> cyc(cus);
+    (void)hipMemcpy(cyc.data(), d_cyc, cus * 8, hipMemcpyDeviceToHost);
+    double c = 0;
+    for (int i = 0; i < cus; i++) c += (double)cyc[i];
+    c /= cus;
+    const double blocks_cu = (double)iters * 64 * W * ILP;
+    const double cyc_per_round = c / (blocks_cu * NR);  // per block-round, per CU
+    const double lds_busy = (blocks_cu * 160.0 / 32.0) / c;
+    const double cfg2_ms = ms * (67.3e6 / (blocks_cu * cus));
+    printf("%-12s ILP %d keys %s waves/CU %2d  %7.3f ms  %6.3f cyc per block-round per CU  LDS busy %.3f  "
+           "cfg2-equiv %.3f ms\n", name, ILP, KEYV ? "VGPR" : "SGPR", W, ms, cyc_per_round, lds_busy, cfg2_ms);
+    fflush(stdout);
+    R r;
+    r.out.resize(nout);
+    (void)hipMemcpy(r.out.data(), d_out, nout * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_cyc);
+    return r;
+}
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? atoi(argv[1]) : 256;  // blocks per lane of the ILP 1 / 16-wave variant
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    uint32_t dk[4 * (NR + 1)];
+    for (int i = 0; i < 4 * (NR + 1); i++) dk[i] = 0x01234567u * (i + 3) ^ (i << 20);
+    uint32_t* d_dk;
+    (void)hipMalloc(&d_dk, sizeof(dk));
+    (void)hipMemcpy(d_dk, dk, sizeof(dk), hipMemcpyHostToDevice);
+    printf("CUs %d\n", cus);
+    const int lanes = 1024;  // blocks in flight per CU of the reference variant
+    std::vector<R> rs;
+    rs.push_back(run<1, 0, 16>("product", d_dk, cus, iters, lanes));
+    rs.push_back(run<1, 1, 16>("keysV", d_dk, cus, iters, lanes));
+    rs.push_back(run<2, 0, 16>("ilp2", d_dk, cus, iters, lanes));
+    rs.push_back(run<2, 1, 16>("ilp2-keysV", d_dk, cus, iters, lanes));
+    rs.push_back(run<2, 0, 8>("ilp2-8w", d_dk, cus, iters, lanes));
+    rs.push_back(run<1, 0, 8>("8w", d_dk, cus, iters, lanes));
+    // variants with the same blocks per CU (64 W x ILP lanes' blocks, decrypted the same number
+    // of times) must agree word for word: product / keysV / ilp2-8w, and ilp2 / ilp2-keysV
+    int bad = 0;
+    if (rs[1].out != rs[0].out || rs[4].out != rs[0].out) {
+        printf("MISMATCH among the 1024-block variants\n");
+        bad = 1;
+    }
+    if (rs[3].out != rs[2].out) {
+        printf("MISMATCH among the 2048-block variants\n");
+        bad = 1;
+    }
+    if (!bad) printf("all variants decrypt the same blocks\n");
+    return bad;
+}

@@ -18,7 +18,10 @@
 #   ab=cfg:rounds:v1,v2,...   tools/ab_bench.sh (variant "base" = the product library)
 #   openab=cfg:rounds:v1,v2,... the open-path rate (bench's open leg, 20 + 5 seal steps) per
 #                      library build, same call ("base" = the product library)
+#   opensplit=cfg:rounds:m1,m2,...  the open leg with each forced split form (auto/chains/blocks/none)
 #   warm               cfg2 value against warmup / timed step counts
+#   mb=<mode>          tools/aes_layout_mb.bin 1027 <mode> (the AES layout microbenchmark; "t": convoy trace)
+#   decmb              tools/aes_dec_mb.bin (the open path's decrypt round loop variants)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
@@ -135,6 +138,20 @@ import json;d=json.load(open('$O/pmc_$c.json'));k=d['dominant_kernel'];v=d['kern
         done
       done
       unset TLSGPU_LIB ;;
+    opensplit)
+      IFS=: read c rounds modes <<< "$arg"
+      for i in $(seq 1 $rounds); do
+        for m in ${modes//,/ }; do
+          run opensplit_${c}_${m}_$i 300 python bench.py --config $c --steps 20 --warmup 5 --no-cpu --no-check --no-host-inclusive --no-derive --open-split $m
+          python3 -c "import json;d=json.loads([l for l in open('$O/opensplit_${c}_${m}_$i.out') if l.startswith('{')][-1]);o=d['open'];print('$c $m open', o['value'], o['ms'], o.get('roundtrip_exact'))"
+        done
+      done ;;
+    decmb)
+      run decmb 300 ./tools/aes_dec_mb.bin 256
+      cat $O/decmb.out ;;
+    mb)
+      run mb_${arg:-all} 300 ./tools/aes_layout_mb.bin 1027 ${arg}
+      cat $O/mb_${arg:-all}.out ;;
     warm)
       for ws in "5 20" "5 50" "500 50" "500 500"; do
         set -- $ws
