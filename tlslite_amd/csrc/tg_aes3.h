@@ -406,11 +406,18 @@ __device__ __forceinline__ uint32_t cbc_group8(const QuadAes& aes, const uint32_
         for (int i = 0; i < 8; i++) f[i] = ld32t<AL>(Pn + 16 * i);
     }
     uint8_t* Ob = O + 16 * b0;
+    // the group's ciphertext is kept and stored at the group's end (round 5, as the pair
+    // kernel's pcbc_group): a chain's eight 16-B pieces of a line reach the L2 together and
+    // merge, instead of one piece per block ~4 us apart, which let partial lines be written
+    // back early and again later (cfg4 PMC: 32.5 GB written for 17.2 GB of wire)
+    uint32_t o[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         iv = aes.encrypt_w<NR, LAT>(__builtin_amdgcn_bitop3_b32(c[i], iv, k[0], 0x96), k);
-        st32t<AL>(Ob + 16 * i, iv);
+        o[i] = iv;
     }
+#pragma unroll
+    for (int i = 0; i < 8; i++) st32t<AL>(Ob + 16 * i, o[i]);
     return iv;
 }
 
@@ -425,10 +432,31 @@ template <int NR, bool LAT, bool AL>
 __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t* k, uint32_t iv,
                                              const uint8_t* P, uint8_t* O, uint32_t nb) {
     if (nb == 0) return iv;
-    const uint32_t last = nb - 1;
+    // Records of at least 16 blocks first run the head blocks up to the output's next 128-B
+    // boundary, so every group stores whole lines (round 5, as pcbc_bulk); the head's loads
+    // are issued with the first group's.
+    uint32_t head = 0;
+    if (nb >= 16) {
+        const uint32_t ob = (uint32_t)(uintptr_t)O & ~15u;  // the block address (lane offset dropped)
+        head = ((128u - (ob & 127u)) & 127u) >> 4;
+    }
+    uint32_t hp[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if ((uint32_t)i < head) hp[i] = ld32t<AL>(P + 16 * i);
+    P += 16 * head;
+    nb -= head;
+    const uint32_t last = nb - 1;  // nb >= 16 - 7 here when head > 0
     uint32_t f[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) f[i] = ld32t<AL>(P + 16 * ((uint32_t)i < last ? (uint32_t)i : last));
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if ((uint32_t)i < head) {
+            iv = aes.encrypt_w<NR, LAT>(__builtin_amdgcn_bitop3_b32(hp[i], iv, k[0], 0x96), k);
+            st32t<AL>(O + 16 * i, iv);
+        }
+    O += 16 * head;
     uint32_t b0 = 0;
     if (nb >= 16) {
         // groups whose refill (blocks b0+8..b0+15) lies inside the record
@@ -568,11 +596,35 @@ __device__ __forceinline__ void pair_block(const PairAes& aes, const uint32_t* k
 constexpr int PAIR_WAVES = 8;
 constexpr int PAIR_WAVES_MANY = CFG_PAIR_WAVES_MANY;  // waves per CU in the many-chains regime
 
+// Issue-priority turns of the pair kernel's waves (round 5).  Two cipher waves share a SIMD
+// (8 waves per CU: w and w + 4), and the SIMD's issue arbiter favours the older one at equal
+// priority: it ran ahead, its partner lagged (per-wave loop time 157 vs 181 cycles per round
+// in tools/aes_layout_microbench.hip's trace mode), and the CU's last rounds ran on the
+// laggards alone.  Taking turns at the higher priority, one G-block group each, keeps the
+// waves of a CU together (168-177 cycles per round): the cfg2-shaped loop 0.911 -> 0.882 ms
+// alone, 0.943 -> 0.864 ms beside a SHA-1 co-runner (profiles/r05/trace_mb.txt).  Both turns
+// stay above the MAC waves' priority (CFG_MAC_PRIO).
+struct PrioTurn {
+    uint32_t turn;  // group count + the wave's SIMD-pair parity
+    __device__ __forceinline__ void init() { turn = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) & 1u; }
+    template <int G>
+    __device__ __forceinline__ void tick() {
+        // one-generation layout (cfg2, 8-block groups): 500 + 500-step cfg2 966 -> 983 GiB/s,
+        // unchanged at 20 + 5; the many-chains form (cfg3, 4-block groups) measured 552 -> 548
+        // (profiles/r05/ab_turns.txt), so it keeps the fixed priority
+        if constexpr (G >= 8) {
+            if (++turn & 1u) __builtin_amdgcn_s_setprio(CFG_CBC_PRIO + 1);
+            else __builtin_amdgcn_s_setprio(CFG_CBC_PRIO);
+        }
+    }
+};
+
 template <int NR, int G, bool AL, bool CLAMP>
 __device__ __forceinline__ void pcbc_group(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
                                            const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
-                                           uint8_t* O, uint32_t b0, uint32_t last, uint2 f[G]) {
+                                           uint8_t* O, uint32_t b0, uint32_t last, uint2 f[G], PrioTurn& turns) {
     constexpr int PAIR_G = G;
+    turns.tick<G>();
     uint2 c[PAIR_G];
 #pragma unroll
     for (int i = 0; i < PAIR_G; i++) c[i] = f[i];
@@ -605,7 +657,7 @@ constexpr uint32_t PAIR_ALIGN_MIN = 16;  // blocks: records this long align thei
 template <int NR, int GI, bool AL>
 __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw, const uint32_t* ka,
                                           const uint32_t* kb, uint32_t& va, uint32_t& vb, const uint8_t* P,
-                                          uint8_t* O, uint32_t nb) {
+                                          uint8_t* O, uint32_t nb, PrioTurn& turns) {
     if (nb == 0) return;
     constexpr uint32_t G = GI;
     // Records of at least PAIR_ALIGN_MIN blocks first run the head blocks up to the output's
@@ -643,12 +695,12 @@ __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw
     if (ng == 0) return;
     uint32_t b0 = 0;
     if (ng >= 2 * G) {  // first group peeled, as cbc_bulk
-        pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, 0, last, f);
+        pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, 0, last, f, turns);
         for (b0 = G; b0 + 2 * G <= ng; b0 += G)
-            pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f);
+            pcbc_group<NR, GI, AL, false>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f, turns);
     }
     if (b0 + G <= ng) {
-        pcbc_group<NR, GI, AL, true>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f);
+        pcbc_group<NR, GI, AL, true>(aes, kw, ka, kb, va, vb, Pg, Og, b0, last, f, turns);
         b0 += G;
     }
 #pragma unroll
@@ -675,6 +727,8 @@ cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const
     __builtin_amdgcn_s_setprio(CFG_CBC_PRIO);
     PairAes aes;
     aes.init();
+    PrioTurn turns;
+    turns.init();
     // persistent over chain generations (as cbc_kernel)
     for (uint32_t cid = blockIdx.x * cpw + local; cid < nchains; cid += gridDim.x * cpw) {
         const tlsgpu_chain ch = chains[cid];
@@ -707,8 +761,8 @@ cbc_pair_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const
             }
             uint8_t* O = B + E + 8 * h;
             const uint32_t nb = n >> 4;
-            if (al) pcbc_bulk<NR, G, true>(aes, kw, ka, kb, va, vb, P, O, nb);
-            else pcbc_bulk<NR, G, false>(aes, kw, ka, kb, va, vb, P, O, nb);
+            if (al) pcbc_bulk<NR, G, true>(aes, kw, ka, kb, va, vb, P, O, nb, turns);
+            else pcbc_bulk<NR, G, false>(aes, kw, ka, kb, va, vb, P, O, nb, turns);
             // tail blocks from the MAC kernel's slot (8-byte aligned)
             const uint32_t r16 = n & 15;
             const uint8_t* slot = tails + (size_t)r * TAIL_SLOT + 8 * h;

@@ -284,7 +284,10 @@ __global__ void __launch_bounds__(1024) bench_kernel(const uint32_t* __restrict_
 
 // Trace kernel (mode "t"): the pair layout of bench_kernel (LAYOUT 2, 256 chains per CU)
 // with per-wave block-start time stamps.  STAGGER 0: no delay; 1: wave w waits w/8 of a
-// round before its loop; 2: odd waves wait half a round.  round_cyc: the delay unit.
+// round before its loop; 2: odd waves wait half a round; 3: no delay, but the two waves of a
+// SIMD (w, w + 4) take turns at the higher issue priority, 8 blocks each (s_setprio 2 / 1),
+// against the age order that otherwise lets the older wave run ahead.  round_cyc: the delay
+// unit.
 constexpr int TR_NS = 64;     // time-stamped blocks per wave
 constexpr int TR_B0 = 200;    // first time-stamped block (the waves have settled by then)
 template <int STAGGER>
@@ -307,7 +310,7 @@ __global__ void __launch_bounds__(512) trace_kernel(const uint32_t* __restrict__
         kb[r] = ek[4 * r + pa + 1];
     }
     uint32_t a = init_word(ch, ca), bb = init_word(ch, ca + 1);
-    if (STAGGER) {
+    if (STAGGER == 1 || STAGGER == 2) {
         const uint64_t d = STAGGER == 1 ? (uint64_t)round_cyc * wave / 8 : (wave & 1) ? (uint64_t)round_cyc / 2 : 0;
         const uint64_t t0 = __builtin_amdgcn_s_memtime();
         while (__builtin_amdgcn_s_memtime() - t0 < d) {
@@ -319,6 +322,10 @@ __global__ void __launch_bounds__(512) trace_kernel(const uint32_t* __restrict__
         if (b >= TR_B0 && b < TR_B0 + TR_NS) {
             const uint64_t t = __builtin_amdgcn_s_memtime();
             if (lane == 0) tr[b - TR_B0] = t;
+        }
+        if (STAGGER == 3 && (b & 7) == 0) {
+            if ((((uint32_t)b >> 3) + (wave >> 2)) & 1) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(1);
         }
         a ^= kwa;
         bb ^= kwb;
@@ -455,7 +462,7 @@ static std::vector<uint32_t> trace_run(const char* name, const uint32_t* d_ek, i
     (void)hipFree(d_out);
     (void)hipFree(d_tr);
     // per wave: round period over the stamped blocks; loop cycles per round
-    double per_sum = 0, loop_sum = 0;
+    double per_sum = 0, loop_sum = 0, loop_min = 1e30, loop_max = 0;
     int hist[10] = {0};
     int npairs = 0;
     double spread_sum = 0;  // per CU and block: max - min block-start over the 8 waves, in rounds
@@ -466,7 +473,10 @@ static std::vector<uint32_t> trace_run(const char* name, const uint32_t* d_ek, i
             const uint64_t* t = &tr[((size_t)c * 8 + w) * (TR_NS + 2)];
             per[w] = (double)(t[TR_NS - 1] - t[0]) / ((TR_NS - 1) * NR);
             per_sum += per[w];
-            loop_sum += (double)(t[TR_NS + 1] - t[TR_NS]) / ((double)blocks * NR);
+            const double lc = (double)(t[TR_NS + 1] - t[TR_NS]) / ((double)blocks * NR);
+            loop_sum += lc;
+            loop_min = lc < loop_min ? lc : loop_min;
+            loop_max = lc > loop_max ? lc : loop_max;
         }
         for (int b = 0; b < TR_NS; b++) {
             uint64_t lo = ~0ull, hi = 0;
@@ -493,10 +503,11 @@ static std::vector<uint32_t> trace_run(const char* name, const uint32_t* d_ek, i
                 }
     }
     const double nw = cus * 8.0;
-    printf("%-10s%s  %7.3f ms (cfg2-equiv %.3f)  round period %6.1f cyc (stamped blocks), loop %6.1f cyc/round  "
-           "block-start spread over the CU's 8 waves %.2f rounds\n  pair phase within a round (10 bins, %% of %d):",
-           name, corun ? " +sha" : "     ", ms, ms * 1027.0 / blocks, per_sum / nw, loop_sum / nw, spread_sum / nspread,
-           npairs);
+    printf("%-10s%s  %7.3f ms (cfg2-equiv %.3f)  round period %6.1f cyc (stamped blocks), loop %6.1f cyc/round "
+           "(waves: min %.1f max %.1f)  block-start spread over the CU's 8 waves %.2f rounds\n  pair phase within a "
+           "round (10 bins, %% of %d):",
+           name, corun ? " +sha" : "     ", ms, ms * 1027.0 / blocks, per_sum / nw, loop_sum / nw, loop_min, loop_max,
+           spread_sum / nspread, npairs);
     for (int k = 0; k < 10; k++) printf(" %4.1f", 100.0 * hist[k] / npairs);
     printf("\n");
     fflush(stdout);
@@ -522,9 +533,11 @@ int main(int argc, char** argv) {
         o.push_back(trace_run<0>("pair1", d_ek, cus, blocks, 0, rc));
         o.push_back(trace_run<1>("pair1-st8", d_ek, cus, blocks, 0, rc));
         o.push_back(trace_run<2>("pair1-st2", d_ek, cus, blocks, 0, rc));
+        o.push_back(trace_run<3>("pair1-alt", d_ek, cus, blocks, 0, rc));
         o.push_back(trace_run<0>("pair1", d_ek, cus, blocks, 2 * blocks, rc));
         o.push_back(trace_run<1>("pair1-st8", d_ek, cus, blocks, 2 * blocks, rc));
         o.push_back(trace_run<2>("pair1-st2", d_ek, cus, blocks, 2 * blocks, rc));
+        o.push_back(trace_run<3>("pair1-alt", d_ek, cus, blocks, 2 * blocks, rc));
         int bad = 0;
         for (size_t i = 1; i < o.size(); i++) bad |= o[i] != o[0];
         printf(bad ? "MISMATCH between trace variants\n" : "all trace variants agree\n");

@@ -22,6 +22,7 @@
 #   warm               cfg2 value against warmup / timed step counts
 #   mb=<mode>          tools/aes_layout_mb.bin 1027 <mode> (the AES layout microbenchmark; "t": convoy trace)
 #   decmb              tools/aes_dec_mb.bin (the open path's decrypt round loop variants)
+#   ldsmb              tools/lds_rate_mb.bin (LDS read rate per CU by read width and waves)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
@@ -146,6 +147,9 @@ import json;d=json.load(open('$O/pmc_$c.json'));k=d['dominant_kernel'];v=d['kern
           python3 -c "import json;d=json.loads([l for l in open('$O/opensplit_${c}_${m}_$i.out') if l.startswith('{')][-1]);o=d['open'];print('$c $m open', o['value'], o['ms'], o.get('roundtrip_exact'))"
         done
       done ;;
+    ldsmb)
+      run ldsmb 300 ./tools/lds_rate_mb.bin 20000
+      cat $O/ldsmb.out ;;
     decmb)
       run decmb 300 ./tools/aes_dec_mb.bin 256
       cat $O/decmb.out ;;
