@@ -284,6 +284,33 @@ def test_unaligned_arenas_vs_oracle(pt_shift, wire_shift, suite, version):
         assert s.seqnum == o.seqnum
 
 
+@pytest.mark.parametrize("pt_shift,wire_shift,suite,version", [(8, 8, "AES128-SHA", (3, 3)),
+                                                                (0, 8, "AES256-SHA", (3, 2)),
+                                                                (4, 12, "AES128-SHA", (3, 1))])
+def test_unaligned_arenas_pair_regime(pt_shift, wire_shift, suite, version):
+    """The pair cipher kernel (>= 256 chains per CU) on arenas off the 16-byte grid: with
+    8-byte-aligned bodies at (wire_off + 5) % 16 == 8 the two lanes of a chain must still
+    agree on the head blocks before the line-aligned groups (round 5 found them computed from
+    the lane's own column address, which differs across the pair there), and 4-byte-aligned
+    arenas take the dword path.  Records of 1-3000 B, one connection each (one launch: one
+    suite per case): every byte equals the oracle."""
+    from oracle import oracle as O
+    from tlslite_amd.device import cu_count
+    T = _T()
+    rng = np.random.default_rng(zlib.crc32(repr(("unal-pair", pt_shift, wire_shift, suite)).encode()))
+    nconn = 256 * cu_count() + 999
+    states, ocs, recs = [], [], []
+    _, kl, ivl, _, ml = O.SUITES[suite]
+    for ci in range(nconn):
+        key, iv, mk, fiv = rng.bytes(kl), rng.bytes(ivl), rng.bytes(ml), rng.bytes(ivl)
+        states.append(T.ConnectionState.for_suite(suite, version, key, iv, mk, fiv, ci))
+        ocs.append(O.Conn.for_suite(suite, version, key, iv, mk, fiv, ci))
+        recs.append((ci, rng.bytes(int(rng.choice([1, 300, 2048, 2999]))), 23, 0))
+    out = T.seal(states, recs, pt_shift=pt_shift, wire_shift=wire_shift)
+    bad = [ci for (ci, p, ct, fl), w in zip(recs, out) if w != ocs[ci].seal(p, ct, fl)]
+    assert not bad, "records differing from the oracle: %d, first %s" % (len(bad), bad[:5])
+
+
 @pytest.mark.parametrize("kind", ["cfg2", "chained", "shuffled", "rc4", "3des"])
 @pytest.mark.parametrize("pinned", [True, False])
 def test_host_pipeline_equals_device_path(kind, pinned):

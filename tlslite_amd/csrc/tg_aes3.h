@@ -437,7 +437,9 @@ __device__ __forceinline__ uint32_t cbc_bulk(const QuadAes& aes, const uint32_t*
     // are issued with the first group's.
     uint32_t head = 0;
     if (nb >= 16) {
-        const uint32_t ob = (uint32_t)(uintptr_t)O & ~15u;  // the block address (lane offset dropped)
+        // the chain's block address, the same in the quad's four lanes (O carries the lane's
+        // column offset 4q; the output need not be 16-byte aligned)
+        const uint32_t ob = (uint32_t)(uintptr_t)O - 4u * (__lane_id() & 3u);
         head = ((128u - (ob & 127u)) & 127u) >> 4;
     }
     uint32_t hp[8];
@@ -669,7 +671,10 @@ __device__ __forceinline__ void pcbc_bulk(const PairAes& aes, const uint32_t* kw
     uint32_t head = 0;
     if (nb >= PAIR_ALIGN_MIN) {
         constexpr uint32_t A = 16 * G;
-        const uint32_t ob = (uint32_t)(uintptr_t)O & ~15u;  // the block address (lane offset dropped)
+        // the chain's block address, the same in both lanes of the pair (O carries the lane's
+        // 8-byte column offset; an 8-byte-aligned output need not be 16-byte aligned: with the
+        // offset masked off instead, the lanes of a pair could pick different heads)
+        const uint32_t ob = (uint32_t)(uintptr_t)O - 8u * (__lane_id() & 1u);
         head = ((A - (ob & (A - 1))) & (A - 1)) >> 4;
         head = head < nb ? head : nb;
     }

@@ -228,6 +228,24 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t first) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// Issue-priority rotation of the decrypt waves (round 5): 16 waves per CU, 4 per SIMD (w,
+// w + 4, w + 8, w + 12), and at equal priority the SIMD's arbiter favours the oldest, so the
+// waves' fixed shares of the work finished far apart (per-wave loop time min / avg / max
+// 0.69 / 1 / 1.33 in tools/aes_dec_microbench.hip) and the CU's last stretch ran on a few
+// waves.  Each wave takes the top priority every fourth chunk: max / avg 1.07, the
+// cfg2-shaped decrypt loop 0.767 -> 0.691 ms (profiles/r05/dec_mb.txt).
+struct PrioRot4 {
+    uint32_t turn;
+    __device__ __forceinline__ void init() { turn = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) & 3u; }
+    __device__ __forceinline__ void tick() {
+        const uint32_t p = ++turn & 3u;
+        if (p == 0) __builtin_amdgcn_s_setprio(3);
+        else if (p == 1) __builtin_amdgcn_s_setprio(2);
+        else if (p == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+    }
+};
+
 // The records a decrypt wave opens, one after another (open_dec_batch's batches of 64
 // candidates, those of this launch's part), with the NEXT record's descriptor and round keys
 // loaded while the current one is decrypted (round 5): lane i holds word i of the next
@@ -299,6 +317,8 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
     uint32_t r = rs.next();
     uint32_t vm = open_fetch_desc(meta, recs, r);
     uint32_t vk = open_fetch_keys<NR>(states, vm, r);
+    PrioRot4 rot;
+    rot.init();
     while (r != ~0u) {
         // this record's descriptor and keys, wave-uniform
         uint32_t dk[4 * (NR + 1)];
@@ -328,6 +348,7 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
             if (lo + lane < hi) load16(C + 16 * (lo + lane), c);
             for (uint32_t base = lo; base < hi; base += 64) {
                 const uint32_t b = base + lane;
+                rot.tick();
                 uint32_t cn[4] = {0, 0, 0, 0};
                 if (b + 64 < hi) load16(C + 16 * (b + 64), cn);  // the next chunk, in flight meanwhile
                 uint32_t p[4];
@@ -422,6 +443,8 @@ open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
     __syncthreads();
     DesLane L;
     L.init();
+    PrioRot4 rot;  // as open_aes_kernel
+    rot.init();
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (OT_THREADS / 64);
@@ -446,6 +469,7 @@ open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
         if (lo + lane < hi) load8(C + 8 * (lo + lane), c);
         for (uint32_t base = lo; base < hi; base += 64) {
             const uint32_t b = base + lane;
+            rot.tick();
             uint32_t cn[2] = {0, 0};
             if (b + 64 < hi) load8(C + 8 * (b + 64), cn);
             uint32_t p[2];

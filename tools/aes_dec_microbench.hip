@@ -20,7 +20,9 @@
 using namespace tg;
 constexpr int NR = 10;
 
-template <int ILP, int KEYV, int W>
+// ROT: the 4 waves of a SIMD (w, w+4, w+8, w+12) rotate the top issue priority every
+// iteration (s_setprio 3..0), against the age order that lets the oldest wave run ahead
+template <int ILP, int KEYV, int W, int ROT = 0>
 __global__ void __launch_bounds__(64 * W, 1) dec_kernel(const uint32_t* __restrict__ dk_g, uint32_t* __restrict__ out,
                                                        uint64_t* __restrict__ cyc, int iters) {
     aes_lds_fill(nullptr, true);
@@ -43,8 +45,16 @@ __global__ void __launch_bounds__(64 * W, 1) dec_kernel(const uint32_t* __restri
     for (int i = 0; i < ILP; i++)
 #pragma unroll
         for (int j = 0; j < 4; j++) s[i][j] = (gid * ILP + i) * 0x9e3779b9u ^ (j * 0x85ebca6bu);
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);  // 0..W/4-1: the wave's rank on its SIMD
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < iters; it++) {
+        if constexpr (ROT) {
+            const uint32_t p = ((uint32_t)it + slot) & 3u;
+            if (p == 0) __builtin_amdgcn_s_setprio(3);
+            else if (p == 1) __builtin_amdgcn_s_setprio(2);
+            else if (p == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
 #pragma unroll
         for (int i = 0; i < ILP; i++) lane_aes_dec<NR>(D, s[i], dkp);
     }
@@ -53,16 +63,16 @@ __global__ void __launch_bounds__(64 * W, 1) dec_kernel(const uint32_t* __restri
     for (int i = 0; i < ILP; i++)
 #pragma unroll
         for (int j = 0; j < 4; j++) out[(gid * ILP + i) * 4 + j] = s[i][j];
-    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+    if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * W + (threadIdx.x >> 6)] = t1 - t0;
 }
 
 struct R {
     std::vector<uint32_t> out;
 };
 
-template <int ILP, int KEYV, int W>
+template <int ILP, int KEYV, int W, int ROT = 0>
 static R run(const char* name, const uint32_t* d_dk, int cus, int iters_total, int lanes_per_cu) {
-    auto kern = dec_kernel<ILP, KEYV, W>;
+    auto kern = dec_kernel<ILP, KEYV, W, ROT>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               AES_DEC_LDS_BYTES);
     // the same blocks in every variant: lanes_per_cu * iters_total blocks per CU, spread as
@@ -72,7 +82,7 @@ static R run(const char* name, const uint32_t* d_dk, int cus, int iters_total, i
     uint32_t* d_out;
     uint64_t* d_cyc;
     (void)hipMalloc(&d_out, nout * 4);
-    (void)hipMalloc(&d_cyc, cus * 8);
+    (void)hipMalloc(&d_cyc, (size_t)cus * W * 8);
     hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * W), AES_DEC_LDS_BYTES, 0, d_dk, d_out, d_cyc, 4);
     (void)hipDeviceSynchronize();
     hipEvent_t e0, e1;
@@ -84,17 +94,24 @@ static R run(const char* name, const uint32_t* d_dk, int cus, int iters_total, i
     (void)hipEventSynchronize(e1);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
-    std::vector<uint64_t> cyc(cus);
-    (void)hipMemcpy(cyc.data(), d_cyc, cus * 8, hipMemcpyDeviceToHost);
-    double c = 0;
-    for (int i = 0; i < cus; i++) c += (double)cyc[i];
-    c /= cus;
+    std::vector<uint64_t> cyc((size_t)cus * W);
+    (void)hipMemcpy(cyc.data(), d_cyc, cyc.size() * 8, hipMemcpyDeviceToHost);
+    double c = 0, cmin = 1e30, cmax = 0;
+    for (size_t i = 0; i < cyc.size(); i++) {
+        c += (double)cyc[i];
+        cmin = (double)cyc[i] < cmin ? (double)cyc[i] : cmin;
+        cmax = (double)cyc[i] > cmax ? (double)cyc[i] : cmax;
+    }
+    c /= cyc.size();
     const double blocks_cu = (double)iters * 64 * W * ILP;
     const double cyc_per_round = c / (blocks_cu * NR);  // per block-round, per CU
     const double lds_busy = (blocks_cu * 160.0 / 32.0) / c;
     const double cfg2_ms = ms * (67.3e6 / (blocks_cu * cus));
-    printf("%-12s ILP %d keys %s waves/CU %2d  %7.3f ms  %6.3f cyc per block-round per CU  LDS busy %.3f  "
-           "cfg2-equiv %.3f ms\n", name, ILP, KEYV ? "VGPR" : "SGPR", W, ms, cyc_per_round, lds_busy, cfg2_ms);
+    printf("%-12s ILP %d keys %s waves/CU %2d  %7.3f ms  cfg2-equiv %.3f ms  per-wave loop (s_memtime cycles) min %.0f "
+           "avg %.0f max %.0f (max/avg %.2f)\n", name, ILP, KEYV ? "VGPR" : "SGPR", W, ms, cfg2_ms, cmin, c, cmax,
+           cmax / c);
+    (void)cyc_per_round;
+    (void)lds_busy;
     fflush(stdout);
     R r;
     r.out.resize(nout);
@@ -123,10 +140,12 @@ int main(int argc, char** argv) {
     rs.push_back(run<2, 1, 16>("ilp2-keysV", d_dk, cus, iters, lanes));
     rs.push_back(run<2, 0, 8>("ilp2-8w", d_dk, cus, iters, lanes));
     rs.push_back(run<1, 0, 8>("8w", d_dk, cus, iters, lanes));
+    rs.push_back(run<1, 0, 16, 1>("product-rot", d_dk, cus, iters, lanes));
+    rs.push_back(run<2, 0, 16, 1>("ilp2-rot", d_dk, cus, iters, lanes));
     // variants with the same blocks per CU (64 W x ILP lanes' blocks, decrypted the same number
     // of times) must agree word for word: product / keysV / ilp2-8w, and ilp2 / ilp2-keysV
     int bad = 0;
-    if (rs[1].out != rs[0].out || rs[4].out != rs[0].out) {
+    if (rs[1].out != rs[0].out || rs[4].out != rs[0].out || rs[6].out != rs[0].out || rs[7].out != rs[2].out) {
         printf("MISMATCH among the 1024-block variants\n");
         bad = 1;
     }
