@@ -334,11 +334,10 @@ int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_o
                     tlsgpu_conn_state *states, uint32_t nstates, int32_t *status, uint32_t variant,
                     void *workspace, size_t workspace_bytes, tlsgpu_stream s);
 /* ABI 6: how CBC-suite opens are split (process-wide).
- * mode TLSGPU_OPEN_SPLIT_AUTO (the default): the library picks from the batch shape;
- * CHAINS / BLOCKS: that form for every batch of at least min_records records (tests);
- * NONE: every pass once on the caller's stream. */
-enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_BLOCKS = 2,
-       TLSGPU_OPEN_SPLIT_NONE = 3 };
+ * mode TLSGPU_OPEN_SPLIT_AUTO (the default): chain-range parts for large batches of short
+ * chains, one pass otherwise; CHAINS: chain-range parts for every batch of at least
+ * min_records records (tests); NONE: every pass once on the caller's stream. */
+enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_NONE = 2 };
 int tlsgpu_set_open_parts(int mode, int64_t min_records);
 /* raw stateful encrypt (decrypt=0) / decrypt (decrypt=1) of spans; one span
  * per state per launch (a state's spans in one launch run in array order). */

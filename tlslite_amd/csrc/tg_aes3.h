@@ -609,14 +609,14 @@ constexpr int PAIR_WAVES_MANY = CFG_PAIR_WAVES_MANY;  // waves per CU in the man
 struct PrioTurn {
     uint32_t turn;  // group count + the wave's SIMD-pair parity
     __device__ __forceinline__ void init() { turn = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) & 1u; }
-    template <int G>
+    template <int G, int BASE = CFG_CBC_PRIO>
     __device__ __forceinline__ void tick() {
         // one-generation layout (cfg2, 8-block groups): 500 + 500-step cfg2 966 -> 983 GiB/s,
         // unchanged at 20 + 5; the many-chains form (cfg3, 4-block groups) measured 552 -> 548
         // (profiles/r05/ab_turns.txt), so it keeps the fixed priority
         if constexpr (G >= 8) {
-            if (++turn & 1u) __builtin_amdgcn_s_setprio(CFG_CBC_PRIO + 1);
-            else __builtin_amdgcn_s_setprio(CFG_CBC_PRIO);
+            if (++turn & 1u) __builtin_amdgcn_s_setprio(BASE + 1);
+            else __builtin_amdgcn_s_setprio(BASE);
         }
     }
 };
@@ -911,6 +911,10 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
     ConnState* st = states + ch.state;
     Des4C D;
     D.init();
+    // the two waves of a SIMD take turns at the higher issue priority, one 8-block group each
+    // (as cbc_pair_kernel: 8 waves per CU, w and w + 4 on one SIMD)
+    PrioTurn turns;
+    turns.init();
     uint32_t b2[48];  // per round: the lane's key / table-base word (Des4C::key2)
 #pragma unroll
     for (int p = 0; p < 3; p++)
@@ -961,6 +965,7 @@ tdes4_kernel(const tlsgpu_chain* __restrict__ chains, uint32_t nchains, const tl
         // (one 64-B piece per chain per group instead of 8 B per block as it completed: the
         // L2 merges whole sectors; cfg5 199.8 -> 210.5 GiB/s, tdes4 5.00 -> 4.74 ms)
         for (; b + 8 <= nb; b += 8) {
+            turns.tick<8, 0>();  // 1 / 0: the RC4 kernel beside it (cfg5) runs at 0
             uint32_t k0 = 0, k1 = 0, k2 = 0, k3 = 0;
 #pragma unroll
             for (int i = 0; i < 8; i++) {

@@ -619,8 +619,7 @@ hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, 
 }
 
 // ---------------------------------------------------------------- open launchers
-// per record: the OpenMeta, and the MAC's hash state between block-range parts
-size_t open_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * (sizeof(OpenMeta) + sizeof(OpenMacState)); }
+size_t open_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * sizeof(OpenMeta); }
 
 // CBC suites (every AES variant: SHA1 TLS/SSL3, SHA256 TLS 1.2; 3DES-SHA) open block-parallel
 static bool open_split_variant(uint32_t v) {
@@ -695,12 +694,14 @@ size_t open_aux_count() {
 // How an open is split (tlsgpu_set_open_parts: tests force each form on small batches).
 //   chain-range parts: large batches of short chains (cfg3: 1 Mi records of one record per
 //     connection) -- OPEN_PARTS ranges of chains, each part's decrypt + padding pass on the
-//     second stream, its MAC pass on the caller's stream beside the next part's decrypt;
-//   block-range parts (round 5): batches of long records (cfg2: 64 Ki x 16 KiB, cfg4) --
-//     every record's tail blocks (the padding) first, then OPEN_PARTS block ranges of every
-//     record on the second stream, the MAC of the payload decrypted so far beside the next
-//     range's decrypt, its hash state kept in the workspace; the last MAC pass finishes.
-enum { OPEN_SPLIT_AUTO = 0, OPEN_SPLIT_CHAINS = 1, OPEN_SPLIT_BLOCKS = 2, OPEN_SPLIT_NONE = 3 };
+//     second stream, its MAC pass on the caller's stream beside the next part's decrypt.
+// (Round 5 also built block-range parts for batches of long records -- every record's tail and
+// padding first, then block ranges of every record with the MAC of the payload decrypted so
+// far beside the next range's decrypt, the hash state carried in the workspace.  They
+// measured slower than one pass on cfg2 (741-745 vs 783-789 GiB/s with the round-5 decrypt;
+// cfg3 230 vs 374-402): every pass re-enters every record, and the part MACs, latency-bound
+// at one wave per SIMD, slowed the decrypt beside them.  Removed; commit 2a0577e has them.)
+enum { OPEN_SPLIT_AUTO = 0, OPEN_SPLIT_CHAINS = 1, OPEN_SPLIT_NONE = 2 };
 static std::atomic<int> open_split_mode{OPEN_SPLIT_AUTO};
 static std::atomic<long long> open_split_min{-1};
 int set_open_parts(int mode, long long min_records) {
@@ -711,16 +712,14 @@ int set_open_parts(int mode, long long min_records) {
 }
 
 // NR 0 = 3DES (8-byte blocks, open_tdes_kernel).  Passes: prefix (caller's stream), then the
-// decrypt / padding / MAC passes in one of the split forms above (or all once on the caller's
-// stream), then the stop pass.
+// decrypt / padding / MAC passes (in chain-range parts, or all once on the caller's stream),
+// then the stop pass.
 template <int NR, int MAC, bool SSL3>
 static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* recs,
                                     uint32_t nrecords, const uint8_t* wire, uint8_t* pt, ConnState* states,
                                     int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, const Bounds& b) {
     constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
-    constexpr int BS = NR == 0 ? 8 : 16;
     OpenMeta* meta = reinterpret_cast<OpenMeta*>(ws);
-    OpenMacState* ms = reinterpret_cast<OpenMacState*>(ws + (size_t)nrecords * sizeof(OpenMeta));
     hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(OpenMeta), s);
     if (e != hipSuccess) return e;
     const dim3 gc((nchains + 255) / 256), gr((nrecords + 255) / 256);
@@ -733,50 +732,42 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
     } else {
         if ((e = set_lds(open_aes_kernel<NR == 0 ? 10 : NR>, AES_DEC_LDS_BYTES, s)) != hipSuccess) return e;
     }
-    // the decrypt (persistent: at most one workgroup per CU) of chains [c0, c1), blocks of `part`
-    auto dec = [&](uint32_t c0, uint32_t c1, uint32_t nrec_part, int part, int nparts, hipStream_t s) {
+    // the decrypt (persistent: at most one workgroup per CU) of chains [c0, c1)
+    auto dec = [&](uint32_t c0, uint32_t c1, uint32_t nrec_part, hipStream_t s) {
         uint32_t grid = (nrec_part + WPB - 1) / WPB;
         grid = grid > ncu ? ncu : (grid ? grid : 1u);
         if constexpr (NR == 0)
             hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire,
-                               pt, states, meta, epoch, c0, c1, part, nparts);
+                               pt, states, meta, epoch, c0, c1);
         else
             hipLaunchKernelGGL(open_aes_kernel<NR == 0 ? 10 : NR>, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s,
-                               recs, nrecords, wire, pt, states, meta, epoch, c0, c1, part, nparts);
+                               recs, nrecords, wire, pt, states, meta, epoch, c0, c1);
     };
     auto seq = [&](uint32_t c0, uint32_t c1, hipStream_t s) {
         hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), dim3((c1 - c0 + 255) / 256), dim3(256), 0, s, chains, nchains,
                            recs, nrecords, pt, states, status, meta, epoch, c0, c1, b.nstates);
     };
-    auto mac = [&](uint32_t c0, uint32_t c1, int part, int nparts, hipStream_t s) {
-        hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3, BS>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status,
-                           meta, ms, epoch, c0, c1, part, nparts);
+    auto mac = [&](uint32_t c0, uint32_t c1, hipStream_t s) {
+        hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status, meta,
+                           epoch, c0, c1);
     };
-    // Which form.  Chain-range parts only when each part's MAC pass alone holds two waves per
-    // SIMD (one lane per record: with fewer records a part's MAC takes as long as the whole
-    // batch's, and four in a row lose -- cfg2: 535-543 vs 733 GiB/s; cfg3, 1 Mi records: 452 vs
-    // 402), and only for short chains (<= 4 records per chain on average: a part's padding pass
-    // walks each chain's records one dependent load after another -- cfg4 587-591 vs 668).
-    // Block-range parts otherwise, when the batch's MAC passes hold at least two waves per CU
-    // (records shorter than the tail -- 17 blocks -- are then decrypted in the tail pass and
-    // hashed in the last MAC pass: the form costs them the extra launches only).
+    // Chain-range parts only when each part's MAC pass alone holds two waves per SIMD (one lane
+    // per record: with fewer records a part's MAC takes as long as the whole batch's, and four
+    // in a row lose -- cfg2: 535-543 vs 733 GiB/s; cfg3, 1 Mi records: 452 vs 402), and only for
+    // short chains (<= 4 records per chain on average: a part's padding pass walks each chain's
+    // records one dependent load after another -- cfg4 587-591 vs 668).
     const int mode_set = open_split_mode.load(std::memory_order_relaxed);
     const long long min_set = open_split_min.load(std::memory_order_relaxed);
-    int mode = OPEN_SPLIT_NONE;
-    if (mode_set == OPEN_SPLIT_AUTO) {
-        if (nchains >= (uint32_t)OPEN_PARTS && nrecords >= (uint64_t)OPEN_PARTS * 512u * ncu &&
-            nrecords <= 4ull * nchains)
-            mode = OPEN_SPLIT_CHAINS;
-        else if (nrecords >= 128u * ncu)
-            mode = OPEN_SPLIT_BLOCKS;
-    } else if (mode_set != OPEN_SPLIT_NONE && nrecords >= (uint64_t)(min_set < 0 ? 0 : min_set) &&
-               (mode_set == OPEN_SPLIT_BLOCKS || nchains >= (uint32_t)OPEN_PARTS)) {
-        mode = mode_set;
-    }
-    if (mode == OPEN_SPLIT_NONE) {
-        dec(0, nchains, nrecords, -1, 0, s);
+    bool parts = false;
+    if (mode_set == OPEN_SPLIT_AUTO)
+        parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= (uint64_t)OPEN_PARTS * 512u * ncu &&
+                nrecords <= 4ull * nchains;
+    else if (mode_set == OPEN_SPLIT_CHAINS)
+        parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= (uint64_t)(min_set < 0 ? 0 : min_set);
+    if (!parts) {
+        dec(0, nchains, nrecords, s);
         seq(0, nchains, s);
-        mac(0u, nchains, -1, 0, s);
+        mac(0u, nchains, s);
     } else {
         std::lock_guard<std::mutex> g(open_aux_mu);
         OpenAux* a = nullptr;
@@ -787,28 +778,14 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
         // waves leave (cfg3 469 vs 454 GiB/s with the MAC passes on the second stream)
         if ((e = hipEventRecord(a->pre_done, s)) != hipSuccess) return e;
         if ((e = hipStreamWaitEvent(a->s2, a->pre_done, 0)) != hipSuccess) return e;
-        if (mode == OPEN_SPLIT_CHAINS) {
-            for (int h = 0; h < OPEN_PARTS; h++) {
-                const uint32_t c0 = (uint32_t)((uint64_t)nchains * h / OPEN_PARTS);
-                const uint32_t c1 = (uint32_t)((uint64_t)nchains * (h + 1) / OPEN_PARTS);
-                dec(c0, c1, nrecords / OPEN_PARTS, -1, 0, a->s2);
-                seq(c0, c1, a->s2);
-                if ((e = hipEventRecord(a->dec_done[h], a->s2)) != hipSuccess) return e;
-                if ((e = hipStreamWaitEvent(s, a->dec_done[h], 0)) != hipSuccess) return e;
-                mac(c0, c1, -1, 0, s);
-            }
-        } else {
-            // tail blocks + padding pass, then block range h of every record beside the MAC of
-            // the payload that ranges < h produced; the last MAC pass hashes the rest and compares
-            dec(0, nchains, nrecords, OPEN_PARTS, OPEN_PARTS, a->s2);
-            seq(0, nchains, a->s2);
-            for (int h = 0; h < OPEN_PARTS; h++) {
-                dec(0, nchains, nrecords, h, OPEN_PARTS, a->s2);
-                if ((e = hipEventRecord(a->dec_done[h], a->s2)) != hipSuccess) return e;
-                if ((e = hipStreamWaitEvent(s, a->dec_done[h], 0)) != hipSuccess) return e;
-                mac(0u, nchains, h, OPEN_PARTS, s);
-            }
-            mac(0u, nchains, OPEN_PARTS, OPEN_PARTS, s);
+        for (int h = 0; h < OPEN_PARTS; h++) {
+            const uint32_t c0 = (uint32_t)((uint64_t)nchains * h / OPEN_PARTS);
+            const uint32_t c1 = (uint32_t)((uint64_t)nchains * (h + 1) / OPEN_PARTS);
+            dec(c0, c1, nrecords / OPEN_PARTS, a->s2);
+            seq(c0, c1, a->s2);
+            if ((e = hipEventRecord(a->dec_done[h], a->s2)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(s, a->dec_done[h], 0)) != hipSuccess) return e;
+            mac(c0, c1, s);
         }
     }
     hipLaunchKernelGGL(open_stop_kernel, gc, dim3(256), 0, s, chains, nchains, recs, nrecords, wire, states, status,
