@@ -16,6 +16,7 @@
 #   profopen=cfg       rocprofv3 --kernel-trace --stats of a short bench run with the open leg -> <tag>/profopen_<cfg>
 #   pmcopen=cfg        tools/pmc_kernels.sh with the open leg -> profiles/pmc_open_<cfg>.json
 #   ab=cfg:rounds:v1,v2,...   tools/ab_bench.sh (variant "base" = the product library)
+#   pmclib=cfg:variant tools/pmc_kernels.sh with an experiment library -> profiles/pmc_<cfg>_<variant>.json
 #   openab=cfg:rounds:v1,v2,... the open-path rate (bench's open leg, 20 + 5 seal steps) per
 #                      library build, same call ("base" = the product library)
 #   opensplit=cfg:rounds:m1,m2,...  the open leg with each forced split form (auto/chains/blocks/none)
@@ -125,6 +126,16 @@ print('open call', d.get('open_call_hbm_bytes'))" ;;
       cp $R/profiles/pmc_$c.json $O/pmc_$c.json
       python3 -c "
 import json;d=json.load(open('$O/pmc_$c.json'));k=d['dominant_kernel'];v=d['kernels'][k];print('$c', k, round(v['duration_ms'],3), 'hbm', v['hbm_bytes'], 'call', d['seal_call_hbm_bytes'])" ;;
+    pmclib)  # pmclib=cfg:variant -- tools/pmc_kernels.sh with tools/ab/<variant>/libtlsgpu.so
+      IFS=: read c v <<< "$arg"
+      TLSGPU_LIB=$R/tools/ab/$v/libtlsgpu.so PMC_NAME=pmc_${c}_$v timeout -k 10 1000 bash tools/pmc_kernels.sh $c $O/pmc_${c}_$v \
+          > $O/pmc_${c}_$v.log 2>&1 || { echo "STEP pmclib $c $v FAILED"; tail -20 $O/pmc_${c}_$v.log; exit 1; }
+      cp $R/profiles/pmc_${c}_$v.json $O/
+      python3 -c "
+import json;d=json.load(open('$O/pmc_${c}_$v.json'))
+for k,v in d['kernels'].items():
+    if v.get('hbm_bytes',0)>1e8: print('$c $v', k[:36], round(v['duration_ms'],3), 'read', v.get('read_bytes'), 'hbm', v['hbm_bytes'])
+print('call', d['seal_call_hbm_bytes'])" ;;
     ab)
       IFS=: read c rounds variants <<< "$arg"
       timeout -k 10 1100 bash tools/ab_bench.sh gpurun_out/$TAG/ab_$c $c $rounds ${variants//,/ } \
