@@ -336,10 +336,8 @@ int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_o
 /* ABI 6: how CBC-suite opens are split (process-wide).
  * mode TLSGPU_OPEN_SPLIT_AUTO (the default): chain-range parts for large batches of short
  * chains, one pass otherwise; CHAINS: chain-range parts for every batch of at least
- * min_records records (tests); NONE: every pass once on the caller's stream; FUSED (AES
- * suites; 3DES opens take NONE): the records' tails and padding first, then the main
- * decrypt and the MAC in one kernel.  AUTO picks FUSED for AES batches it does not split. */
-enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_NONE = 2, TLSGPU_OPEN_SPLIT_FUSED = 3 };
+ * min_records records (tests); NONE: every pass once on the caller's stream. */
+enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_NONE = 2 };
 int tlsgpu_set_open_parts(int mode, int64_t min_records);
 /* raw stateful encrypt (decrypt=0) / decrypt (decrypt=1) of spans; one span
  * per state per launch (a state's spans in one launch run in array order). */

@@ -30,7 +30,5 @@ constexpr int CFG_PAIR_G1 = 8;
 constexpr int CFG_PAIR_GM = 4;
 // seal pipeline: workspaces in rotation (the MAC stream may run PIPE_WS - 1 calls ahead)
 constexpr int CFG_PIPE_WS = 3;
-// open_fused_kernel: the MAC waves' issue priority (the decrypt waves rotate 0..3)
-constexpr int CFG_OPEN_MAC_PRIO = 1;
 
 }  // namespace tg

@@ -619,10 +619,7 @@ hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, 
 }
 
 // ---------------------------------------------------------------- open launchers
-// one OpenMeta per record, then the fused open's per-workgroup stripe counters
-size_t open_workspace_bytes(uint32_t nrecords) {
-    return (size_t)nrecords * sizeof(OpenMeta) + (size_t)OF_MAX_CTL * sizeof(OpenFusedCtl);
-}
+size_t open_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * sizeof(OpenMeta); }
 
 // CBC suites (every AES variant: SHA1 TLS/SSL3, SHA256 TLS 1.2; 3DES-SHA) open block-parallel
 static bool open_split_variant(uint32_t v) {
@@ -698,20 +695,22 @@ size_t open_aux_count() {
 //   chain-range parts: large batches of short chains (cfg3: 1 Mi records of one record per
 //     connection) -- OPEN_PARTS ranges of chains, each part's decrypt + padding pass on the
 //     second stream, its MAC pass on the caller's stream beside the next part's decrypt.
-//   fused (AES): the records' tails decrypted first (open_aes_kernel<NR, true>), the padding
-//     pass, then open_fused_kernel -- decrypt and MAC waves in one workgroup per CU.
-//   none: one decrypt pass, the padding pass, one MAC pass.
 // (Round 5 also built block-range parts for batches of long records -- every record's tail and
 // padding first, then block ranges of every record with the MAC of the payload decrypted so
 // far beside the next range's decrypt, the hash state carried in the workspace.  They
 // measured slower than one pass on cfg2 (741-745 vs 783-789 GiB/s with the round-5 decrypt;
 // cfg3 230 vs 374-402): every pass re-enters every record, and the part MACs, latency-bound
-// at one wave per SIMD, slowed the decrypt beside them.  Removed; commit 2a0577e has them.)
-enum { OPEN_SPLIT_AUTO = 0, OPEN_SPLIT_CHAINS = 1, OPEN_SPLIT_NONE = 2, OPEN_SPLIT_FUSED = 3 };
+// at one wave per SIMD, slowed the decrypt beside them.  Removed; commit 2a0577e has them.
+// Round 5 then fused the two: 12 decrypt waves and 4 MAC waves per workgroup, the MAC hashing
+// each 64-block stripe of 256 records as soon as the decrypt waves publish it.  Its timeline
+// (profiles/r05/trace_open_fused.txt) shows every stripe's decrypt slowed by the full MAC time
+// beside it -- the two share the SIMDs' issue, so overlapping them saves nothing: cfg2
+// 675-684 vs 781-806 GiB/s.  Removed; commit ce9d3c2 has it.)
+enum { OPEN_SPLIT_AUTO = 0, OPEN_SPLIT_CHAINS = 1, OPEN_SPLIT_NONE = 2 };
 static std::atomic<int> open_split_mode{OPEN_SPLIT_AUTO};
 static std::atomic<long long> open_split_min{-1};
 int set_open_parts(int mode, long long min_records) {
-    if (mode < OPEN_SPLIT_AUTO || mode > OPEN_SPLIT_FUSED) return -1;
+    if (mode < OPEN_SPLIT_AUTO || mode > OPEN_SPLIT_NONE) return -1;
     open_split_mode.store(mode, std::memory_order_relaxed);
     open_split_min.store(min_records < 0 ? -1 : min_records, std::memory_order_relaxed);
     return 0;
@@ -726,8 +725,7 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
                                     int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, const Bounds& b) {
     constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
     OpenMeta* meta = reinterpret_cast<OpenMeta*>(ws);
-    OpenFusedCtl* ctl = reinterpret_cast<OpenFusedCtl*>(ws + (size_t)nrecords * sizeof(OpenMeta));
-    hipError_t e = hipMemsetAsync(meta, 0, open_workspace_bytes(nrecords), s);
+    hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(OpenMeta), s);
     if (e != hipSuccess) return e;
     const dim3 gc((nchains + 255) / 256), gr((nrecords + 255) / 256);
     hipLaunchKernelGGL((open_prefix_kernel<CID, MAC, SSL3>), gc, dim3(256), 0, s, chains, nchains, recs, nrecords,
@@ -737,10 +735,7 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
     if (NR == 0) {
         if ((e = set_lds(open_tdes_kernel, DES_LDS_BYTES, s)) != hipSuccess) return e;
     } else {
-        if ((e = set_lds(open_aes_kernel<NR == 0 ? 10 : NR, false>, AES_DEC_LDS_BYTES, s)) != hipSuccess) return e;
-        if ((e = set_lds(open_aes_kernel<NR == 0 ? 10 : NR, true>, AES_DEC_LDS_BYTES, s)) != hipSuccess) return e;
-        if ((e = set_lds(open_fused_kernel<NR == 0 ? 10 : NR, MAC, SSL3>, AES_DEC_LDS_BYTES, s)) != hipSuccess)
-            return e;
+        if ((e = set_lds(open_aes_kernel<NR == 0 ? 10 : NR>, AES_DEC_LDS_BYTES, s)) != hipSuccess) return e;
     }
     // the decrypt (persistent: at most one workgroup per CU) of chains [c0, c1)
     auto dec = [&](uint32_t c0, uint32_t c1, uint32_t nrec_part, hipStream_t s) {
@@ -750,8 +745,8 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
             hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire,
                                pt, states, meta, epoch, c0, c1);
         else
-            hipLaunchKernelGGL((open_aes_kernel<NR == 0 ? 10 : NR, false>), dim3(grid), dim3(O3_THREADS),
-                               AES_DEC_LDS_BYTES, s, recs, nrecords, wire, pt, states, meta, epoch, c0, c1);
+            hipLaunchKernelGGL(open_aes_kernel<NR == 0 ? 10 : NR>, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s,
+                               recs, nrecords, wire, pt, states, meta, epoch, c0, c1);
     };
     auto seq = [&](uint32_t c0, uint32_t c1, hipStream_t s) {
         hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), dim3((c1 - c0 + 255) / 256), dim3(256), 0, s, chains, nchains,
@@ -768,30 +763,13 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
     // records one dependent load after another -- cfg4 587-591 vs 668).
     const int mode_set = open_split_mode.load(std::memory_order_relaxed);
     const long long min_set = open_split_min.load(std::memory_order_relaxed);
-    bool parts = false, fused = false;
-    if (mode_set == OPEN_SPLIT_AUTO) {
+    bool parts = false;
+    if (mode_set == OPEN_SPLIT_AUTO)
         parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= (uint64_t)OPEN_PARTS * 512u * ncu &&
                 nrecords <= 4ull * nchains;
-        fused = !parts && NR != 0;
-    } else if (mode_set == OPEN_SPLIT_CHAINS) {
+    else if (mode_set == OPEN_SPLIT_CHAINS)
         parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= (uint64_t)(min_set < 0 ? 0 : min_set);
-    } else if (mode_set == OPEN_SPLIT_FUSED) {
-        fused = NR != 0;
-    }
-    if (fused) {
-        if constexpr (NR != 0) {
-            uint32_t grid = (nrecords + WPB - 1) / WPB;
-            grid = grid > ncu ? ncu : (grid ? grid : 1u);
-            hipLaunchKernelGGL((open_aes_kernel<NR, true>), dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s, recs,
-                               nrecords, wire, pt, states, meta, epoch, 0u, nchains);
-            seq(0, nchains, s);
-            uint32_t fg = (nrecords + OF_GEN - 1) / OF_GEN;
-            fg = fg > ncu ? ncu : fg;
-            fg = fg > OF_MAX_CTL ? OF_MAX_CTL : (fg ? fg : 1u);
-            hipLaunchKernelGGL((open_fused_kernel<NR, MAC, SSL3>), dim3(fg), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s,
-                               recs, nrecords, wire, pt, states, status, meta, ctl, epoch);
-        }
-    } else if (!parts) {
+    if (!parts) {
         dec(0, nchains, nrecords, s);
         seq(0, nchains, s);
         mac(0u, nchains, s);

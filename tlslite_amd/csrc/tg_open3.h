@@ -252,59 +252,13 @@ __device__ __forceinline__ uint32_t open_fetch_keys(const ConnState* states, uin
     return 0u;
 }
 
-// CBC-decrypt blocks [lo, hi) of one record with one wave, 64 blocks (one 1 KiB chunk) at a
-// time, carry = C_{lo-1} (wave-uniform).  Round 5: the next chunk's ciphertext is loaded
-// before the current one is decrypted (its HBM latency hides under the chunk's ten rounds
-// instead of stalling the wave at every chunk), and a lane's predecessor block C_{b-1} is its
-// left neighbour's ciphertext, moved over by DPP (wave_shr:1) -- only lane 0 takes it from
-// the previous chunk's lane 63 (readlane) or `carry`, instead of every lane loading the block
-// again.  after_first() runs once, after the first chunk (the caller's prefetch hook).
-template <int NR, class F>
-__device__ __forceinline__ void dec_range(const QuadAesDec& D, const uint32_t* dk, const uint8_t* C, uint8_t* P,
-                                          uint32_t E, uint32_t lo, uint32_t hi, uint32_t carry[4], PrioRot4& rot,
-                                          F&& after_first) {
-    const uint32_t lane = __lane_id();
-    uint32_t c[4] = {0, 0, 0, 0};
-    if (lo + lane < hi) load16(C + 16 * (lo + lane), c);
-    bool first = true;
-    for (uint32_t base = lo; base < hi; base += 64) {
-        const uint32_t b = base + lane;
-        rot.tick();
-        uint32_t cn[4] = {0, 0, 0, 0};
-        if (b + 64 < hi) load16(C + 16 * (b + 64), cn);  // the next chunk, in flight meanwhile
-        uint32_t p[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            p[i] = wave_shr1(c[i], carry[i]);
-            carry[i] = __builtin_amdgcn_readlane(c[i], 63);  // the next chunk's lane-0 predecessor
-        }
-        if (b < hi) {
-            uint32_t d[4] = {c[0], c[1], c[2], c[3]};
-            lane_aes_dec<NR>(D, d, dk);
-#pragma unroll
-            for (int i = 0; i < 4; i++) d[i] ^= p[i];
-            if (16 * b >= E) store16(P + 16 * b - E, d);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++) c[i] = cn[i];
-        if (first) {
-            after_first();
-            first = false;
-        }
-    }
-    if (first) after_first();
-}
-
-// AES open: the tail of every record -- its last OPEN_TAIL blocks, which hold every padding
-// byte (tlsrecordlayer.py:979-993: up to 255 + 1 bytes) -- decrypted first, so the padding
-// pass and with it the MAC's length field are known before open_fused_kernel hashes the
-// payload as its decrypt waves produce it (round 5).
-constexpr uint32_t OPEN_TAIL = 256u / 16u + 1u;
-__device__ __forceinline__ uint32_t open_main_blocks(uint32_t nb) { return nb > OPEN_TAIL ? nb - OPEN_TAIL : 0u; }
-
-// TAIL false: every block of every record (one pass, or chain-range parts); TAIL true: blocks
-// [open_main_blocks(nb), nb) of every record (the fused open's first pass).
-template <int NR, bool TAIL>
+// A wave walks one record 64 blocks (one 1 KiB chunk) at a time.  Round 5: the next chunk's ciphertext is loaded before the current
+// one is decrypted (its HBM latency hides under the chunk's ten rounds instead of stalling the
+// wave at every chunk), and a lane's predecessor block C_{b-1} is its left neighbour's
+// ciphertext, moved over by DPP (wave_shr:1) -- only lane 0 takes it from the previous
+// chunk's lane 63 (readlane) or the record's first predecessor (OpenMeta.pred), instead of
+// every lane loading the block again.
+template <int NR>
 __global__ void __launch_bounds__(O3_THREADS, 1)
 open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
                 uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
@@ -313,6 +267,7 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
     __syncthreads();
     QuadAesDec D;
     D.init();
+    const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     OpenDecStream rs;
     rs.meta = meta;
@@ -345,275 +300,42 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
         // the next record's descriptor now; its keys after this record's first chunk
         const uint32_t rn = rs.next();
         vm = open_fetch_desc(meta, recs, rn);
+        bool keys_pending = true;
         const uint32_t nb = ct_len >> 4;
         const uint8_t* C = wire + ct_off;
-        const uint32_t lo = TAIL ? open_main_blocks(nb) : 0u;
-        if (lo) load16(C + 16 * (lo - 1), carry);  // wave-uniform: the block before the tail
-        dec_range<NR>(D, dk, C, pt + pt_off, E, lo, nb, carry, rot,
-                      [&] { vk = open_fetch_keys<NR>(states, vm, rn); });
-        r = rn;
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// open_fused_kernel (round 5): the AES open's main decrypt and its MAC in ONE kernel, so the
-// MAC -- one lane per record, latency-bound at one wave per SIMD when it runs alone (cfg2:
-// 0.39 of 1.35 ms) -- hashes a record's payload while its later blocks are still being
-// decrypted.  One 1024-thread workgroup per CU (persistent): 12 decrypt waves (the Td / InvS
-// tables fill the CU's LDS) and 4 MAC waves, one lane per record, over generations of 256
-// records.  A generation's decrypt goes stripe by stripe -- stripe s = blocks [64 s, 64 s + 64)
-// of every record of the generation, before its tail (decrypted already by
-// open_aes_kernel<NR, true>) -- decrypt wave w taking records w, w + 12, ... of the
-// generation; a wave publishes a stripe once its stores are complete (release fence, then an
-// atomic add on the workgroup's counter for that stripe).  A MAC wave waits until all 12
-// decrypt waves have published stripe s (acquire), then hashes the payload chunks stripes
-// 0..s have produced; after its records' last stripe it hashes the rest, finishes and
-// compares (open_mac_kernel's arithmetic).  Counters are cumulative per generation parity
-// (every decrypt wave publishes all OF_MAX_STRIPES stripes of every generation, so stripe s
-// of the workgroup's j-th generation is complete at 12 (j / 2 + 1)): nothing is reset and the
-// decrypt waves never wait -- the only wait is MAC on decrypt inside one workgroup, whose 16
-// waves are co-resident.  Every wait has a watchdog (~1 s): a MAC wave that times out reports
-// TLSGPU_EHIP for its records instead of hanging the device.
-constexpr int OF_DEC_WAVES = 12, OF_MAC_WAVES = 4, OF_GEN = 64 * OF_MAC_WAVES;
-constexpr int OF_RECS_PER_WAVE = (OF_GEN + OF_DEC_WAVES - 1) / OF_DEC_WAVES;  // 22
-constexpr int OF_MAX_STRIPES = 20;  // 18 432-byte ciphertexts (tlsrecordlayer's cap): 1152 blocks
-struct OpenFusedCtl {
-    uint32_t cnt[2][OF_MAX_STRIPES];
-    uint32_t pad[64 - 2 * OF_MAX_STRIPES];  // one per workgroup, 256 B apart
-};
-static_assert(sizeof(OpenFusedCtl) == 256, "OpenFusedCtl");
-constexpr uint32_t OF_MAX_CTL = 256;  // workgroups (the workspace holds this many controls)
-
-// A decrypt wave's records of one generation, one per lane (lane i: record w + 12 i), and the
-// (stripe, record) items it walks: stripe by stripe, the records that have main blocks there.
-struct OfDecGen {
-    uint32_t ct_lo, ct_hi, pt_lo, pt_hi, main, st, E, pred[4];  // lane-held
-    uint32_t s, S;
-    uint64_t mask;
-    __device__ __forceinline__ void load(const tlsgpu_open_record* recs, const ConnState* states,
-                                         const OpenMeta* meta, uint32_t nrecords, uint32_t epoch, uint32_t gen_base,
-                                         uint32_t wv) {
-        const uint32_t lane = __lane_id();
-        const uint32_t k = wv + (uint32_t)OF_DEC_WAVES * lane, r = gen_base + k;
-        main = 0;
-        ct_lo = ct_hi = pt_lo = pt_hi = st = E = 0;
-        pred[0] = pred[1] = pred[2] = pred[3] = 0;
-        if (lane < (uint32_t)OF_RECS_PER_WAVE && k < (uint32_t)OF_GEN && r < nrecords) {
-            const OpenMeta mt = meta[r];
-            if (mt.epoch == epoch && (mt.flags & OM_DEC)) {
-                const tlsgpu_open_record R = recs[r];
-                ct_lo = (uint32_t)R.ct_off;
-                ct_hi = (uint32_t)(R.ct_off >> 32);
-                pt_lo = (uint32_t)R.pt_off;
-                pt_hi = (uint32_t)(R.pt_off >> 32);
-                main = open_main_blocks(R.ct_len >> 4);
-                st = mt.state;
-                E = states[mt.state].explicit_iv ? 16u : 0u;
-#pragma unroll
-                for (int i = 0; i < 4; i++) pred[i] = mt.pred[i];
-            }
-        }
-        uint32_t m = (main + 63u) >> 6;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-        S = __builtin_amdgcn_readfirstlane(m);
-        s = 0;
-        mask = S ? __ballot(main > 0) : 0ull;
-    }
-    // the next item: (stripe, lane of its record), or false at the generation's end
-    __device__ __forceinline__ bool next(uint32_t& is, uint32_t& il) {
-        while (!mask) {
-            if (++s >= S) return false;
-            mask = __ballot(main > 64u * s);
-        }
-        is = s;
-        il = (uint32_t)__builtin_ctzll(mask);
-        mask &= mask - 1;
-        return true;
-    }
-};
-
-// One item in flight: its record's lane-held words, ciphertext chunk and the block before it
-// (wave-uniform), loaded one item ahead; its round keys are scalar loads at the item's start,
-// from a scalar cache warmed one item ahead (a v_readlane per key word from a prefetched VGPR
-// adds ~15 % VALU to a chunk's decrypt, and two key sets in SGPRs spill).
-struct OfItem {
-    uint32_t s, il, lo, hi, E;
-    uint64_t ct, pt;
-    const uint32_t* kp;  // the record's equivalent-inverse round keys
-    uint32_t w[4];       // one word of each 64-byte line of them: the scalar cache warmed
-    uint32_t c[4], carry[4];
-    bool ok;
-};
-template <int NR>
-__device__ __forceinline__ void of_fetch(OfItem& it, OfDecGen& g, const uint8_t* wire, const ConnState* states) {
-    it.ok = g.next(it.s, it.il);
-    if (!it.ok) return;
-    const uint32_t lane = __lane_id();
-    const uint32_t il = it.il;
-    it.ct = (uint64_t)__builtin_amdgcn_readlane(g.ct_lo, il) | ((uint64_t)__builtin_amdgcn_readlane(g.ct_hi, il) << 32);
-    it.pt = (uint64_t)__builtin_amdgcn_readlane(g.pt_lo, il) | ((uint64_t)__builtin_amdgcn_readlane(g.pt_hi, il) << 32);
-    it.E = __builtin_amdgcn_readlane(g.E, il);
-    it.lo = 64u * it.s;
-    it.hi = min(it.lo + 64u, __builtin_amdgcn_readlane(g.main, il));
-    it.kp = states[__builtin_amdgcn_readlane(g.st, il)].dk;
-    it.w[0] = it.kp[0];
-    it.w[1] = it.kp[16];
-    it.w[2] = it.kp[32];
-    it.w[3] = it.kp[4 * (NR + 1) - 1];
-    const uint8_t* C = wire + it.ct;
-    it.c[0] = it.c[1] = it.c[2] = it.c[3] = 0;
-    if (it.lo + lane < it.hi) load16(C + 16 * (it.lo + lane), it.c);
-    if (it.lo) {
-        load16(C + 16 * (it.lo - 1), it.carry);  // one address for all lanes
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; i++) it.carry[i] = __builtin_amdgcn_readlane(g.pred[i], il);
-    }
-}
-
-template <int NR, int MAC, bool SSL3>
-__global__ void __launch_bounds__(O3_THREADS, 1)
-open_fused_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
-                  uint8_t* __restrict__ pt, const ConnState* __restrict__ states, int32_t* __restrict__ status,
-                  const OpenMeta* __restrict__ meta, OpenFusedCtl* __restrict__ ctl, uint32_t epoch) {
-    aes_lds_fill(nullptr, true);
-    __syncthreads();
-    const uint32_t lane = __lane_id();
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    OpenFusedCtl* C = ctl + blockIdx.x;
-    if (wv < (uint32_t)OF_DEC_WAVES) {
-        // ---- decrypt waves
-        QuadAesDec D;
-        D.init();
-        PrioRot4 rot;  // three decrypt waves per SIMD (slots 0..2) rotate four levels
-        rot.init();
-        for (uint32_t j = 0;; j++) {
-            const uint32_t gen_base = (j * gridDim.x + blockIdx.x) * (uint32_t)OF_GEN;
-            if (gen_base >= nrecords) break;
-            const uint32_t par = j & 1u;
-            OfDecGen g;
-            g.load(recs, states, meta, nrecords, epoch, gen_base, wv);
-            uint32_t pub = 0;  // stripes [0, pub) published
-            OfItem cur;
-            of_fetch<NR>(cur, g, wire, states);
-            while (cur.ok) {
+        uint8_t* P = pt + pt_off;
+        const uint32_t hi = nb;
+        {
+            uint32_t c[4] = {0, 0, 0, 0};
+            if (lane < hi) load16(C + 16 * lane, c);
+            for (uint32_t base = 0; base < hi; base += 64) {
+                const uint32_t b = base + lane;
                 rot.tick();
-                uint32_t dk[4 * (NR + 1)];
-#pragma unroll
-                for (int i = 0; i < 4 * (NR + 1); i++) dk[i] = cur.kp[i];
-                asm volatile("" ::"s"(cur.w[0]), "s"(cur.w[1]), "s"(cur.w[2]), "s"(cur.w[3]));
-                const uint32_t b = cur.lo + lane;
-                uint32_t p[4], d[4];
+                uint32_t cn[4] = {0, 0, 0, 0};
+                if (b + 64 < hi) load16(C + 16 * (b + 64), cn);  // the next chunk, in flight meanwhile
+                uint32_t p[4];
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
-                    p[i] = wave_shr1(cur.c[i], cur.carry[i]);
-                    d[i] = cur.c[i];
+                    p[i] = wave_shr1(c[i], carry[i]);
+                    carry[i] = __builtin_amdgcn_readlane(c[i], 63);  // the next chunk's lane-0 predecessor
                 }
-                const uint32_t hi = cur.hi, E = cur.E, s = cur.s;
-                uint8_t* P = pt + cur.pt;
-                OfItem nx;
-                of_fetch<NR>(nx, g, wire, states);  // the next item, in flight meanwhile
-                lane_aes_dec<NR>(D, d, dk);
+                if (b < hi) {
+                    uint32_t d[4] = {c[0], c[1], c[2], c[3]};
+                    lane_aes_dec<NR>(D, d, dk);
 #pragma unroll
-                for (int i = 0; i < 4; i++) d[i] ^= p[i];
-                // publish the stripes before this item's: their stores were issued an item ago
-                if (pub < s) {
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    if (lane == 0)
-                        for (uint32_t t = pub; t < s; t++)
-                            __hip_atomic_fetch_add(&C->cnt[par][t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    pub = s;
+                    for (int i = 0; i < 4; i++) d[i] ^= p[i];
+                    if (16 * b >= E) store16(P + 16 * b - E, d);
                 }
-                if (b < hi && 16 * b >= E) store16(P + 16 * b - E, d);
-                cur = nx;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0)
-                for (uint32_t t = pub; t < (uint32_t)OF_MAX_STRIPES; t++)
-                    __hip_atomic_fetch_add(&C->cnt[par][t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
-    // ---- MAC waves: lane = one record of the generation
-    __builtin_amdgcn_s_setprio(CFG_OPEN_MAC_PRIO);
-    using M = RecMac<MAC, SSL3>;
-    constexpr int DL = M::DL;
-    const uint32_t k = (wv - OF_DEC_WAVES) * 64u + lane;
-    for (uint32_t j = 0;; j++) {
-        const uint32_t gen_base = (j * gridDim.x + blockIdx.x) * (uint32_t)OF_GEN;
-        if (gen_base >= nrecords) break;
-        const uint32_t par = j & 1u;
-        const uint32_t target = (uint32_t)OF_DEC_WAVES * (j / 2u + 1u);
-        const uint32_t r = gen_base + k;
-        OpenMeta mt = {};
-        tlsgpu_open_record R = {};
-        bool act = r < nrecords;
-        if (act) {
-            mt = meta[r];
-            act = mt.epoch == epoch && (mt.flags & OM_VERIFY);
-        }
-        if (act) R = recs[r];
-        const ConnState* st = states + (act ? mt.state : 0u);
-        const uint8_t* P = pt + R.pt_off;
-        const uint32_t n = act ? mt.n : 0u, nfull = n >> 6;
-        const uint32_t E = act && st->explicit_iv ? 16u : 0u;
-        const uint32_t main = act ? open_main_blocks(R.ct_len >> 4) : 0u;
-        uint32_t Sw = (main + 63u) >> 6;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) Sw = max(Sw, (uint32_t)__shfl_xor((int)Sw, o));
-        Sw = __builtin_amdgcn_readfirstlane(Sw);
-        M mac;
-        if (act) mac.begin(st, mt.seq, R.content_type, n);
-        uint32_t done = 0;
-        bool timed_out = false;
-        for (uint32_t s = 0; s < Sw; s++) {
-            // wait for stripe s of this generation (watchdog ~1 s)
-            uint32_t seen = 0;
-            for (uint32_t it = 0; it < (1u << 23); it++) {
-                seen = __hip_atomic_load(&C->cnt[par][s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                seen = __builtin_amdgcn_readfirstlane(seen);
-                if (seen >= target) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-            if (seen < target) {
-                timed_out = true;
-                break;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the CU's L1 invalidated (lines read before the stripe was stored)
-            if (act) {
-                // payload chunks whose bytes stripes 0..s (and the tail) have produced
-                const uint32_t front = 64u * (s + 1u);
-                uint32_t ready = nfull;
-                if (front < main) {
-                    const uint32_t bytes = 16u * front > E ? 16u * front - E : 0u;
-                    ready = min(nfull, bytes >> 6);
-                }
-                if (ready > done) {
-                    if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, P + 64 * done, ready - done);
-                    else mac_bulk<false>(mac, P + 64 * done, ready - done);
-                    done = ready;
+                for (int i = 0; i < 4; i++) c[i] = cn[i];
+                if (keys_pending) {
+                    vk = open_fetch_keys<NR>(states, vm, rn);
+                    keys_pending = false;
                 }
             }
         }
-        if (timed_out) {
-            if (act) status[r] = TLSGPU_EHIP;
-            continue;
-        }
-        if (!act) continue;
-        if (nfull > done) {  // records with no main blocks (all tail)
-            if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, P + 64 * done, nfull - done);
-            else mac_bulk<false>(mac, P + 64 * done, nfull - done);
-        }
-        uint32_t tail[16];
-        load_partial(P + 64 * nfull, n & 63, tail);
-        uint32_t m[8];
-        mac.finish(tail, (int)(n & 63), n, st, m);
-        bool macGood = true;
-#pragma unroll
-        for (int i = 0; i < DL; i++)
-            if (P[n + i] != (uint8_t)(m[i >> 2] >> (8 * (i & 3)))) macGood = false;
-        status[r] = ((mt.flags & OM_PADOK) && macGood) ? (int32_t)n : TLSGPU_ALERT_BAD_RECORD_MAC;
+        if (keys_pending) vk = open_fetch_keys<NR>(states, vm, rn);
+        r = rn;
     }
 }
 
