@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--host-inclusive", dest="host_inclusive", action="store_true",
                     help="measure the PCIe-inclusive rate (default: cfg2 only -- cfg4's 16 GiB arenas would "
                          "pin 32 GiB of host memory for it)")
-    ap.add_argument("--open-split", default=None, choices=["auto", "chains", "none"],
+    ap.add_argument("--open-split", default=None, choices=["auto", "chains", "none", "blocks"],
                     help="force the open path's split form (tlsgpu_set_open_parts; default: the library's choice)")
     ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -763,7 +763,7 @@ def main():
             if args.open_split:
                 from tlslite_amd.recordlayer import set_open_parts
                 set_open_parts({"auto": N.OPEN_SPLIT_AUTO, "chains": N.OPEN_SPLIT_CHAINS,
-                                "none": N.OPEN_SPLIT_NONE}[args.open_split], 0)
+                                "none": N.OPEN_SPLIT_NONE, "blocks": N.OPEN_SPLIT_BLOCKS}[args.open_split], 0)
             open_res = open_rate(wl, stream, args.steps)
             if args.open_split:
                 open_res["split"] = args.open_split

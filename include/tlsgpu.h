@@ -336,8 +336,13 @@ int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_o
 /* ABI 6: how CBC-suite opens are split (process-wide).
  * mode TLSGPU_OPEN_SPLIT_AUTO (the default): chain-range parts for large batches of short
  * chains, one pass otherwise; CHAINS: chain-range parts for every batch of at least
- * min_records records (tests); NONE: every pass once on the caller's stream. */
-enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_NONE = 2 };
+ * min_records records (tests); NONE: every pass once on the caller's stream; BLOCKS (3DES
+ * suites; AES opens take NONE): block-range parts -- every record's tail and the padding
+ * pass first, then block ranges of every record beside the MAC of the payload decrypted so
+ * far -- for every batch of at least min_records records.  AUTO picks BLOCKS for 3DES
+ * batches of >= 128 records per CU that it does not split by chain. */
+enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_NONE = 2,
+       TLSGPU_OPEN_SPLIT_BLOCKS = 3 };
 int tlsgpu_set_open_parts(int mode, int64_t min_records);
 /* raw stateful encrypt (decrypt=0) / decrypt (decrypt=1) of spans; one span
  * per state per launch (a state's spans in one launch run in array order). */

@@ -274,14 +274,18 @@ def test_stop_on_alert_like_connection(suite, version):
                                                 ("3DES-SHA", (3, 1), "chains"), ("AES128-SHA", (3, 0), "chains"),
                                                 ("AES128-SHA", (3, 3), "single"), ("AES256-SHA256", (3, 3), "single"),
                                                 ("3DES-SHA", (3, 2), "single"), ("AES128-SHA", (3, 0), "single"),
-                                                ("AES256-SHA", (3, 1), "single")])
+                                                ("AES256-SHA", (3, 1), "single"), ("3DES-SHA", (3, 2), "blocks"),
+                                                ("3DES-SHA", (3, 0), "blocks"), ("3DES-SHA", (3, 1), "blocks")])
 def test_split_open_parts_like_oracle(suite, version, mode):
     """The open's forms (launch_open_split; tlsgpu_set_open_parts forces them on these small
     batches).  "chains": in parts on a second stream, the decrypt and padding pass of chain
     range h+1 beside the MAC pass of range h -- 6,000 connections of 1-6 records of 1-700 B.
     "single": one pass of each kernel on long records (the round-5 decrypt: next record's
     keys prefetched, DPP predecessors, wave priority rotation, byte-replicated inverse
-    S-box) -- 900 connections of 1-4 records of 1 B-16 KiB.  ~3 % of records tampered (a bit
+    S-box) -- 900 connections of 1-4 records of 1 B-16 KiB.  "blocks" (3DES): the same records
+    with every record's tail blocks and the padding pass first, then block range h+1 of every
+    record beside the MAC of the payload ranges <= h produced, the hash state carried in the
+    workspace, so records end in every part.  ~3 % of records tampered (a bit
     flipped anywhere: payload, MAC or padding) or truncated, connection (stop-on-alert)
     semantics: every status, plaintext and final state equals the oracle's, across the part
     boundaries (tlsrecordlayer.py:958-1044)."""
@@ -314,7 +318,7 @@ def test_split_open_parts_like_oracle(suite, version, mode):
         elif u < 0.03:
             body = body[:-1]
         recs.append((ci, ct, bytes(body)))
-    set_open_parts(N.OPEN_SPLIT_CHAINS if mode == "chains" else N.OPEN_SPLIT_NONE, 1)
+    set_open_parts({"chains": N.OPEN_SPLIT_CHAINS, "single": N.OPEN_SPLIT_NONE, "blocks": N.OPEN_SPLIT_BLOCKS}[mode], 1)
     try:
         res = open_records(readers, recs)
     finally:

@@ -17,7 +17,7 @@ FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
 OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH = 0, -1, -2, -3, -4, -5
 ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED, ALERT_SKIPPED = -20, -21, -22
 CHAIN_STOP_ON_ALERT = 1
-OPEN_SPLIT_AUTO, OPEN_SPLIT_CHAINS, OPEN_SPLIT_NONE = 0, 1, 2
+OPEN_SPLIT_AUTO, OPEN_SPLIT_CHAINS, OPEN_SPLIT_NONE, OPEN_SPLIT_BLOCKS = 0, 1, 2, 3
 ABI_VERSION = 6
 CONN_STATE_BYTES = 2048
 

@@ -350,7 +350,7 @@ size_t tlsgpu_owned_workspace_count(void) {
 size_t tlsgpu_owned_stream_count(void) { return open_aux_count(); }
 
 int tlsgpu_set_open_parts(int mode, int64_t min_records) {
-    if (set_open_parts(mode, min_records) != 0) return fail(TLSGPU_EINVAL, "open split mode must be 0..2");
+    if (set_open_parts(mode, min_records) != 0) return fail(TLSGPU_EINVAL, "open split mode must be 0..3");
     return 0;
 }
 

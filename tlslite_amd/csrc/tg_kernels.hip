@@ -619,7 +619,8 @@ hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, 
 }
 
 // ---------------------------------------------------------------- open launchers
-size_t open_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * sizeof(OpenMeta); }
+// per record: the OpenMeta, and the MAC's hash state between block-range parts
+size_t open_workspace_bytes(uint32_t nrecords) { return (size_t)nrecords * (sizeof(OpenMeta) + sizeof(OpenMacState)); }
 
 // CBC suites (every AES variant: SHA1 TLS/SSL3, SHA256 TLS 1.2; 3DES-SHA) open block-parallel
 static bool open_split_variant(uint32_t v) {
@@ -695,10 +696,13 @@ size_t open_aux_count() {
 //   chain-range parts: large batches of short chains (cfg3: 1 Mi records of one record per
 //     connection) -- OPEN_PARTS ranges of chains, each part's decrypt + padding pass on the
 //     second stream, its MAC pass on the caller's stream beside the next part's decrypt.
-// (Round 5 also built block-range parts for batches of long records -- every record's tail and
-// padding first, then block ranges of every record with the MAC of the payload decrypted so
-// far beside the next range's decrypt, the hash state carried in the workspace.  They
-// measured slower than one pass on cfg2 (741-745 vs 783-789 GiB/s with the round-5 decrypt;
+//   block-range parts (3DES suites): every record's tail blocks (the padding) first, then
+//     OPEN_PARTS block ranges of every record on the second stream, the MAC of the payload
+//     decrypted so far beside the next range's decrypt, its hash state kept in the
+//     workspace; the last MAC pass finishes.  The 3DES decrypt (48 Feistel rounds of 8 SP
+//     lookups per 8-byte block) leaves the SIMDs' VALU issue to the MAC beside it: cfg5 open
+//     310-314 vs 268-272 GiB/s in one pass (profiles/r05/ab_open.txt).
+// (For AES, round 5 measured the block-range parts slower than one pass on cfg2 (741-745 vs 783-789 GiB/s with the round-5 decrypt;
 // cfg3 230 vs 374-402): every pass re-enters every record, and the part MACs, latency-bound
 // at one wave per SIMD, slowed the decrypt beside them.  Removed; commit 2a0577e has them.
 // Round 5 then fused the two: 12 decrypt waves and 4 MAC waves per workgroup, the MAC hashing
@@ -706,11 +710,11 @@ size_t open_aux_count() {
 // (profiles/r05/trace_open_fused.txt) shows every stripe's decrypt slowed by the full MAC time
 // beside it -- the two share the SIMDs' issue, so overlapping them saves nothing: cfg2
 // 675-684 vs 781-806 GiB/s.  Removed; commit ce9d3c2 has it.)
-enum { OPEN_SPLIT_AUTO = 0, OPEN_SPLIT_CHAINS = 1, OPEN_SPLIT_NONE = 2 };
+enum { OPEN_SPLIT_AUTO = 0, OPEN_SPLIT_CHAINS = 1, OPEN_SPLIT_NONE = 2, OPEN_SPLIT_BLOCKS = 3 };
 static std::atomic<int> open_split_mode{OPEN_SPLIT_AUTO};
 static std::atomic<long long> open_split_min{-1};
 int set_open_parts(int mode, long long min_records) {
-    if (mode < OPEN_SPLIT_AUTO || mode > OPEN_SPLIT_NONE) return -1;
+    if (mode < OPEN_SPLIT_AUTO || mode > OPEN_SPLIT_BLOCKS) return -1;
     open_split_mode.store(mode, std::memory_order_relaxed);
     open_split_min.store(min_records < 0 ? -1 : min_records, std::memory_order_relaxed);
     return 0;
@@ -724,7 +728,9 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
                                     uint32_t nrecords, const uint8_t* wire, uint8_t* pt, ConnState* states,
                                     int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, const Bounds& b) {
     constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
+    constexpr int BS = NR == 0 ? 8 : 16;
     OpenMeta* meta = reinterpret_cast<OpenMeta*>(ws);
+    OpenMacState* ms = reinterpret_cast<OpenMacState*>(ws + (size_t)nrecords * sizeof(OpenMeta));
     hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(OpenMeta), s);
     if (e != hipSuccess) return e;
     const dim3 gc((nchains + 255) / 256), gr((nrecords + 255) / 256);
@@ -738,12 +744,13 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
         if ((e = set_lds(open_aes_kernel<NR == 0 ? 10 : NR>, AES_DEC_LDS_BYTES, s)) != hipSuccess) return e;
     }
     // the decrypt (persistent: at most one workgroup per CU) of chains [c0, c1)
-    auto dec = [&](uint32_t c0, uint32_t c1, uint32_t nrec_part, hipStream_t s) {
+    // (3DES: blocks of block-range part `part` of `nparts`, every block when part < 0)
+    auto dec = [&](uint32_t c0, uint32_t c1, uint32_t nrec_part, hipStream_t s, int part = -1, int nparts = 0) {
         uint32_t grid = (nrec_part + WPB - 1) / WPB;
         grid = grid > ncu ? ncu : (grid ? grid : 1u);
         if constexpr (NR == 0)
             hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire,
-                               pt, states, meta, epoch, c0, c1);
+                               pt, states, meta, epoch, c0, c1, part, nparts);
         else
             hipLaunchKernelGGL(open_aes_kernel<NR == 0 ? 10 : NR>, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s,
                                recs, nrecords, wire, pt, states, meta, epoch, c0, c1);
@@ -752,9 +759,9 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
         hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), dim3((c1 - c0 + 255) / 256), dim3(256), 0, s, chains, nchains,
                            recs, nrecords, pt, states, status, meta, epoch, c0, c1, b.nstates);
     };
-    auto mac = [&](uint32_t c0, uint32_t c1, hipStream_t s) {
-        hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status, meta,
-                           epoch, c0, c1);
+    auto mac = [&](uint32_t c0, uint32_t c1, hipStream_t s, int part = -1, int nparts = 0) {
+        hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3, BS>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status,
+                           meta, ms, epoch, c0, c1, part, nparts);
     };
     // Chain-range parts only when each part's MAC pass alone holds two waves per SIMD (one lane
     // per record: with fewer records a part's MAC takes as long as the whole batch's, and four
@@ -763,16 +770,41 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
     // records one dependent load after another -- cfg4 587-591 vs 668).
     const int mode_set = open_split_mode.load(std::memory_order_relaxed);
     const long long min_set = open_split_min.load(std::memory_order_relaxed);
-    bool parts = false;
-    if (mode_set == OPEN_SPLIT_AUTO)
-        parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= (uint64_t)OPEN_PARTS * 512u * ncu &&
-                nrecords <= 4ull * nchains;
-    else if (mode_set == OPEN_SPLIT_CHAINS)
-        parts = nchains >= (uint32_t)OPEN_PARTS && nrecords >= (uint64_t)(min_set < 0 ? 0 : min_set);
-    if (!parts) {
+    // Block-range parts (3DES only) when the batch's MAC passes hold at least two waves per CU.
+    int mode = OPEN_SPLIT_NONE;
+    const uint64_t min_rec = (uint64_t)(min_set < 0 ? 0 : min_set);
+    if (mode_set == OPEN_SPLIT_AUTO) {
+        if (nchains >= (uint32_t)OPEN_PARTS && nrecords >= (uint64_t)OPEN_PARTS * 512u * ncu &&
+            nrecords <= 4ull * nchains)
+            mode = OPEN_SPLIT_CHAINS;
+        else if (NR == 0 && nrecords >= 128u * ncu)
+            mode = OPEN_SPLIT_BLOCKS;
+    } else if (mode_set == OPEN_SPLIT_CHAINS) {
+        if (nchains >= (uint32_t)OPEN_PARTS && nrecords >= min_rec) mode = OPEN_SPLIT_CHAINS;
+    } else if (mode_set == OPEN_SPLIT_BLOCKS) {
+        if (NR == 0 && nrecords >= min_rec) mode = OPEN_SPLIT_BLOCKS;
+    }
+    if (mode == OPEN_SPLIT_NONE) {
         dec(0, nchains, nrecords, s);
         seq(0, nchains, s);
         mac(0u, nchains, s);
+    } else if (mode == OPEN_SPLIT_BLOCKS) {
+        std::lock_guard<std::mutex> g(open_aux_mu);
+        OpenAux* a = nullptr;
+        if ((e = open_aux(s, &a)) != hipSuccess) return e;
+        if ((e = hipEventRecord(a->pre_done, s)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(a->s2, a->pre_done, 0)) != hipSuccess) return e;
+        // tail blocks + padding pass, then block range h of every record beside the MAC of the
+        // payload that ranges < h produced; the last MAC pass hashes the rest and compares
+        dec(0, nchains, nrecords, a->s2, OPEN_PARTS, OPEN_PARTS);
+        seq(0, nchains, a->s2);
+        for (int h = 0; h < OPEN_PARTS; h++) {
+            dec(0, nchains, nrecords, a->s2, h, OPEN_PARTS);
+            if ((e = hipEventRecord(a->dec_done[h], a->s2)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(s, a->dec_done[h], 0)) != hipSuccess) return e;
+            mac(0u, nchains, s, h, OPEN_PARTS);
+        }
+        mac(0u, nchains, s, OPEN_PARTS, OPEN_PARTS);
     } else {
         std::lock_guard<std::mutex> g(open_aux_mu);
         OpenAux* a = nullptr;

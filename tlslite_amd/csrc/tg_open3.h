@@ -24,13 +24,14 @@
 //                       what the failing record left (the reference closes the
 //                       connection at the alert, :1039-1042).
 //
-// Workspace per record: one 48-byte OpenMeta.
+// Workspace per record: one 48-byte OpenMeta and one 48-byte OpenMacState.
 //
-// A large open runs in parts by chain range (launch_open_split): the decrypt and
-// padding pass of part h+1 on the library's second stream beside the MAC pass of part h
-// on the caller's stream -- the decrypt is LDS-bound, the MAC VALU-bound.  Each kernel after
-// the prefix takes the part's chain range [c_lo, c_hi) and skips records of other
-// chains (OpenMeta.chain).
+// A large open runs in parts (launch_open_split), the decrypt (and padding) pass of part h+1
+// on the library's second stream beside the MAC pass of part h on the caller's stream: by
+// chain range for batches of short chains (each kernel after the prefix takes the part's
+// chain range [c_lo, c_hi) and skips records of other chains, OpenMeta.chain), by block range
+// for 3DES batches (every record's tail first, then block ranges of every record; the MAC
+// passes carry the hash state in OpenMacState).
 #pragma once
 #include "tg_aes3.h"
 
@@ -49,6 +50,41 @@ struct OpenMeta {
 static_assert(sizeof(OpenMeta) == 48, "OpenMeta");
 constexpr uint32_t OM_DEC = 1, OM_VERIFY = 2, OM_PADOK = 4;
 constexpr int O3_THREADS = 1024;
+
+// The hash state of a record's MAC between the passes of an open in block-range parts
+// (launch_open_split, 3DES suites): RecMac's h[] and its window tail prev[].
+struct OpenMacState {
+    uint32_t h[8];
+    uint32_t prev[4];
+};
+static_assert(sizeof(OpenMacState) == 48, "OpenMacState");
+
+// Ciphertext blocks [lo, hi) of a record of nb blocks that pass `part` of an open in
+// `nparts` block-range parts decrypts:
+//   part < 0        every block (an open in one pass, or in chain-range parts);
+//   part == nparts  the tail: the last 256 / BS + 1 blocks, which hold every padding byte
+//                   (tlsrecordlayer.py:979-993: up to 255 + 1 bytes), decrypted first so
+//                   that the padding pass -- and with it the MAC's length field -- is
+//                   known before the first MAC part;
+//   part h          the h-th of nparts 64-block-aligned pieces of the blocks before the tail.
+template <uint32_t BS>
+__device__ __forceinline__ void open_part_blocks(uint32_t nb, int part, int nparts, uint32_t& lo, uint32_t& hi) {
+    constexpr uint32_t TB = 256u / BS + 1u;
+    if (part < 0) {
+        lo = 0;
+        hi = nb;
+        return;
+    }
+    const uint32_t tail = nb > TB ? nb - TB : 0u;
+    if (part >= nparts) {
+        lo = tail;
+        hi = nb;
+        return;
+    }
+    const uint32_t chunks = (tail + 63u) >> 6;
+    lo = min(tail, 64u * (chunks * (uint32_t)part / (uint32_t)nparts));
+    hi = min(tail, 64u * (chunks * (uint32_t)(part + 1) / (uint32_t)nparts));
+}
 
 // LDS addressing of the equivalent-inverse-cipher tables (FIPS-197 5.3.5,
 // rijndael.py:321-362): the Td tables in the encryption tables' layout (aes_lds_fill with
@@ -399,15 +435,14 @@ struct DesLane {
 __global__ void __launch_bounds__(OT_THREADS, 1)
 open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, const uint8_t* __restrict__ wire,
                  uint8_t* __restrict__ pt, const ConnState* __restrict__ states, const OpenMeta* __restrict__ meta,
-                 uint32_t epoch, uint32_t c_lo, uint32_t c_hi) {
+                 uint32_t epoch, uint32_t c_lo, uint32_t c_hi, int part, int nparts) {
     extern __shared__ __attribute__((aligned(16))) uint32_t ot_lds[];
     des_lds_fill(ot_lds);  // the kernel's only LDS: the tables start at LDS byte 0
     __syncthreads();
     DesLane L;
     L.init();
-    // (no priority rotation here, unlike open_aes_kernel: cfg5 opens its 3DES records beside
-    // the RC4 lane-per-chain kernel on another stream, and decrypt waves above its priority
-    // slowed the pair: 337.5 -> 309.2 GiB/s, profiles/r05/ab_open.txt)
+    // (no priority rotation here, unlike open_aes_kernel: on cfg5 it measured neutral, 268-271
+    // vs 270-272 GiB/s, profiles/r05/ab_open.txt)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t nwaves = gridDim.x * (OT_THREADS / 64);
@@ -422,12 +457,16 @@ open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
         const uint32_t nb = R.ct_len >> 3;
         const uint8_t* C = wire + R.ct_off;
         uint8_t* P = pt + R.pt_off;
-        // next chunk prefetched, predecessor from the left neighbour (as open_aes_kernel)
-        const uint32_t hi = nb;
+        // next chunk prefetched, predecessor from the left neighbour (as open_aes_kernel); the
+        // blocks of this pass (open_part_blocks)
+        uint32_t lo, hi;
+        open_part_blocks<8>(nb, part, nparts, lo, hi);
+        if (lo >= hi) continue;
         uint32_t carry[2] = {mt.pred[0], mt.pred[1]};
+        if (lo) load8(C + 8 * (lo - 1), carry);  // wave-uniform: the block before this pass's first
         uint32_t c[2] = {0, 0};
-        if (lane < hi) load8(C + 8 * lane, c);
-        for (uint32_t base = 0; base < hi; base += 64) {
+        if (lo + lane < hi) load8(C + 8 * (lo + lane), c);
+        for (uint32_t base = lo; base < hi; base += 64) {
             const uint32_t b = base + lane;
             uint32_t cn[2] = {0, 0};
             if (b + 64 < hi) load8(C + 8 * (b + 64), cn);
@@ -504,13 +543,26 @@ __global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __res
 // round 4: cfg2 718 vs 733, cfg3 397 vs 402 GiB/s -- with one lane per 16 KiB record the
 // open's MAC is latency-bound, and the transposes sit on that path;
 // profiles/r04/ab/ab_open_r04.txt.)
-template <int MAC, bool SSL3>
+// part < 0: the whole MAC in one pass.  Block-range parts (3DES): pass h < nparts hashes
+// the payload chunks whose blocks the decrypt parts 0..h (and the tail) have produced and
+// keeps the hash state in the workspace (OpenMacState); pass nparts hashes the rest,
+// finishes and compares.
+template <int BS>
+__device__ __forceinline__ uint32_t open_chunks_ready(uint32_t nb, uint32_t E, uint32_t nfull, int part, int nparts) {
+    uint32_t lo, hi;
+    open_part_blocks<BS>(nb, part, nparts, lo, hi);
+    const uint32_t bytes = BS * hi > E ? BS * hi - E : 0u;  // payload bytes decrypted from its start
+    return min(nfull, bytes >> 6);
+}
+
+template <int MAC, bool SSL3, int BS>
 __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
                                                       const uint8_t* __restrict__ pt,
                                                       const ConnState* __restrict__ states,
                                                       int32_t* __restrict__ status,
-                                                      const OpenMeta* __restrict__ meta, uint32_t epoch,
-                                                      uint32_t c_lo, uint32_t c_hi) {
+                                                      const OpenMeta* __restrict__ meta, OpenMacState* __restrict__ ms,
+                                                      uint32_t epoch, uint32_t c_lo, uint32_t c_hi, int part,
+                                                      int nparts) {
     using M = RecMac<MAC, SSL3>;
     constexpr int DL = M::DL;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -522,11 +574,35 @@ __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record*
     const tlsgpu_open_record R = recs[r];
     const uint8_t* P = pt + R.pt_off;
     const uint32_t n = mt.n;
-    M mac;
-    mac.begin(st, mt.seq, R.content_type, n);
     const uint32_t nfull = n >> 6;
-    if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, P, nfull);
-    else mac_bulk<false>(mac, P, nfull);
+    M mac;
+    uint32_t c0 = 0, c1 = nfull;
+    if (part >= 0) {
+        const uint32_t E = st->explicit_iv ? (uint32_t)BS : 0u;
+        const uint32_t nb = R.ct_len / BS;
+        c0 = part == 0 ? 0u : open_chunks_ready<BS>(nb, E, nfull, part - 1, nparts);
+        c1 = part == nparts ? nfull : open_chunks_ready<BS>(nb, E, nfull, part, nparts);
+    }
+    if (c0 == 0) {
+        mac.begin(st, mt.seq, R.content_type, n);
+    } else {
+        const OpenMacState& q = ms[r];
+#pragma unroll
+        for (int k = 0; k < 8; k++) mac.h[k] = q.h[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) mac.prev[k] = q.prev[k];
+    }
+    const uint8_t* Pc = P + 64 * c0;
+    if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, Pc, c1 - c0);
+    else mac_bulk<false>(mac, Pc, c1 - c0);
+    if (part >= 0 && part < nparts) {  // more parts follow: keep the hash state
+        OpenMacState& q = ms[r];
+#pragma unroll
+        for (int k = 0; k < 8; k++) q.h[k] = mac.h[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) q.prev[k] = mac.prev[k];
+        return;
+    }
     uint32_t tail[16];
     load_partial(P + 64 * nfull, n & 63, tail);
     uint32_t m[8];

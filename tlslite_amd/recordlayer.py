@@ -350,7 +350,8 @@ def open_dev(chains, nchains, records, nrecords, wire, pt, states, status, varia
 def set_open_parts(mode=N.OPEN_SPLIT_AUTO, min_records=0):
     """How CBC-suite opens are split (process-wide): N.OPEN_SPLIT_AUTO (the library picks),
     N.OPEN_SPLIT_CHAINS (chain-range parts for every batch of >= min_records records: tests
-    run the form on small batches), N.OPEN_SPLIT_NONE (one pass each)."""
+    run the form on small batches), N.OPEN_SPLIT_NONE (one pass each), N.OPEN_SPLIT_BLOCKS
+    (3DES: block-range parts for every batch of >= min_records records)."""
     N.call("tlsgpu_set_open_parts", int(mode), int(min_records))
 
 
