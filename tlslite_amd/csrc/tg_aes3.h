@@ -613,7 +613,7 @@ struct PrioTurn {
     __device__ __forceinline__ void tick() {
         // one-generation layout (cfg2, 8-block groups): 500 + 500-step cfg2 966 -> 983 GiB/s,
         // unchanged at 20 + 5; the many-chains form (cfg3, 4-block groups) measured 552 -> 548
-        // (profiles/r05/ab_turns.txt), so it keeps the fixed priority
+        // (profiles/r05/ab_seal.txt), so it keeps the fixed priority
         if constexpr (G >= 8) {
             if (++turn & 1u) __builtin_amdgcn_s_setprio(BASE + 1);
             else __builtin_amdgcn_s_setprio(BASE);
