@@ -60,6 +60,25 @@ def test_abi_structs_and_constants():
     assert [f[0] for f in N.Chain._fields_] == ["state", "first", "count", "flags"]
 
 
+def test_open_split_modes_match_header():
+    """tlsgpu_set_open_parts: the header's TLSGPU_OPEN_SPLIT_* values equal the bindings'
+    constants, every mode is accepted and anything else is refused with TLSGPU_EINVAL (host
+    only: no GPU needed); the open workspace holds an OpenMeta and an OpenMacState per record."""
+    from tlslite_amd import _native as N
+    src = open(os.path.join(ROOT, "include", "tlsgpu.h")).read()
+    for name, val in [("AUTO", N.OPEN_SPLIT_AUTO), ("CHAINS", N.OPEN_SPLIT_CHAINS), ("NONE", N.OPEN_SPLIT_NONE),
+                      ("BLOCKS", N.OPEN_SPLIT_BLOCKS)]:
+        assert re.search(r"\bTLSGPU_OPEN_SPLIT_%s\s*=\s*%d\b" % (name, val), src), name
+    try:
+        for m in (N.OPEN_SPLIT_AUTO, N.OPEN_SPLIT_CHAINS, N.OPEN_SPLIT_NONE, N.OPEN_SPLIT_BLOCKS):
+            assert N.lib.tlsgpu_set_open_parts(m, 0) == 0, m
+        for bad in (-1, 4, 99):
+            assert N.lib.tlsgpu_set_open_parts(bad, 0) == N.EINVAL, bad
+    finally:
+        assert N.lib.tlsgpu_set_open_parts(N.OPEN_SPLIT_AUTO, -1) == 0
+    assert N.lib.tlsgpu_open_workspace_bytes(1000) == 1000 * 96
+
+
 def test_state_validation_mirrors_reference():
     from tlslite_amd import ConnectionState, _native as N
     ok = ConnectionState("aes128", "sha1", (3, 3), bytes(16), bytes(16), bytes(20), bytes(16))
