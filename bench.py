@@ -808,6 +808,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": wl.dominant_kernel(), "kernel_avg_ms": round(avg_ms, 4),
+                         # the timed steps' kernel times in order: a short run's first steps run
+                         # at the clocks of a GPU that has just started working
+                         "kernel_ms_steps": {"first": round(per_launch[0], 4),
+                                             "median": round(float(np.median(per_launch)), 4),
+                                             "last": round(per_launch[-1], 4),
+                                             "min": round(min(per_launch), 4), "max": round(max(per_launch), 4)},
                          "alg_bytes_per_launch": alg_bytes,
                          "batch_alg_bytes": wl.plaintext_total + wl.wire_total,
                          "copy_measured": round(copy_gbs, 1),
