@@ -20,11 +20,42 @@
 using namespace tg;
 constexpr int NR = 10;
 
+// GL: lookups served by the vector memory path (a 2 KiB table in global memory, L1-resident)
+// instead of LDS, to spread the gather load over two pipes: 1 = the last round's inverse
+// S-box (16 of 160 lookups per block), 2 = that and every round's Td3 lookups (56 of 160)
+template <int NR, int GL>
+__device__ __forceinline__ void lane_aes_dec_gl(const QuadAesDec& D, uint32_t s[4], const uint32_t* dk,
+                                                const uint32_t* __restrict__ g) {
+    const QuadAes& A = D.t;
+    uint32_t s0 = s[0] ^ dk[0], s1 = s[1] ^ dk[1], s2 = s[2] ^ dk[2], s3 = s[3] ^ dk[3];
+    auto t3 = [&](uint32_t x) -> uint32_t {
+        if constexpr (GL >= 2) return g[x >> 24];
+        else return A.look<3, 3>(x);
+    };
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        const uint32_t* k = dk + 4 * r;
+        const uint32_t t0 = bx3(bx3(A.look<0, 0>(s0), A.look<1, 1>(s3), A.look<2, 2>(s2)), t3(s1), k[0]);
+        const uint32_t t1 = bx3(bx3(A.look<0, 0>(s1), A.look<1, 1>(s0), A.look<2, 2>(s3)), t3(s2), k[1]);
+        const uint32_t t2 = bx3(bx3(A.look<0, 0>(s2), A.look<1, 1>(s1), A.look<2, 2>(s0)), t3(s3), k[2]);
+        const uint32_t t3v = bx3(bx3(A.look<0, 0>(s3), A.look<1, 1>(s2), A.look<2, 2>(s1)), t3(s0), k[3]);
+        s0 = t0; s1 = t1; s2 = t2; s3 = t3v;
+    }
+    const uint32_t* k = dk + 4 * NR;
+    const uint32_t* gi = g + 256;
+    auto ib = [&](uint32_t x, int B) -> uint32_t { return gi[(x >> (8 * B)) & 0xffu]; };
+    s[0] = QuadAesDec::col(ib(s0, 0), ib(s3, 1), ib(s2, 2), ib(s1, 3), k[0]);
+    s[1] = QuadAesDec::col(ib(s1, 0), ib(s0, 1), ib(s3, 2), ib(s2, 3), k[1]);
+    s[2] = QuadAesDec::col(ib(s2, 0), ib(s1, 1), ib(s0, 2), ib(s3, 3), k[2]);
+    s[3] = QuadAesDec::col(ib(s3, 0), ib(s2, 1), ib(s1, 2), ib(s0, 3), k[3]);
+}
+
 // ROT: the 4 waves of a SIMD (w, w+4, w+8, w+12) rotate the top issue priority every
 // iteration (s_setprio 3..0), against the age order that lets the oldest wave run ahead
-template <int ILP, int KEYV, int W, int ROT = 0>
+template <int ILP, int KEYV, int W, int ROT = 0, int GL = 0>
 __global__ void __launch_bounds__(64 * W, 1) dec_kernel(const uint32_t* __restrict__ dk_g, uint32_t* __restrict__ out,
-                                                       uint64_t* __restrict__ cyc, int iters) {
+                                                       uint64_t* __restrict__ cyc, int iters,
+                                                       const uint32_t* __restrict__ gtab) {
     aes_lds_fill(nullptr, true);
     __syncthreads();
     QuadAesDec D;
@@ -56,7 +87,10 @@ __global__ void __launch_bounds__(64 * W, 1) dec_kernel(const uint32_t* __restri
             else __builtin_amdgcn_s_setprio(0);
         }
 #pragma unroll
-        for (int i = 0; i < ILP; i++) lane_aes_dec<NR>(D, s[i], dkp);
+        for (int i = 0; i < ILP; i++) {
+            if constexpr (GL) lane_aes_dec_gl<NR, GL>(D, s[i], dkp, gtab);
+            else lane_aes_dec<NR>(D, s[i], dkp);
+        }
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
 #pragma unroll
@@ -70,9 +104,10 @@ struct R {
     std::vector<uint32_t> out;
 };
 
-template <int ILP, int KEYV, int W, int ROT = 0>
+static const uint32_t* g_gtab = nullptr;
+template <int ILP, int KEYV, int W, int ROT = 0, int GL = 0>
 static R run(const char* name, const uint32_t* d_dk, int cus, int iters_total, int lanes_per_cu) {
-    auto kern = dec_kernel<ILP, KEYV, W, ROT>;
+    auto kern = dec_kernel<ILP, KEYV, W, ROT, GL>;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               AES_DEC_LDS_BYTES);
     // the same blocks in every variant: lanes_per_cu * iters_total blocks per CU, spread as
@@ -83,13 +118,13 @@ static R run(const char* name, const uint32_t* d_dk, int cus, int iters_total, i
     uint64_t* d_cyc;
     (void)hipMalloc(&d_out, nout * 4);
     (void)hipMalloc(&d_cyc, (size_t)cus * W * 8);
-    hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * W), AES_DEC_LDS_BYTES, 0, d_dk, d_out, d_cyc, 4);
+    hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * W), AES_DEC_LDS_BYTES, 0, d_dk, d_out, d_cyc, 4, g_gtab);
     (void)hipDeviceSynchronize();
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0);
-    hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * W), AES_DEC_LDS_BYTES, 0, d_dk, d_out, d_cyc, iters);
+    hipLaunchKernelGGL(kern, dim3(cus), dim3(64 * W), AES_DEC_LDS_BYTES, 0, d_dk, d_out, d_cyc, iters, g_gtab);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms = 0;
@@ -132,6 +167,19 @@ int main(int argc, char** argv) {
     (void)hipMalloc(&d_dk, sizeof(dk));
     (void)hipMemcpy(d_dk, dk, sizeof(dk), hipMemcpyHostToDevice);
     printf("CUs %d\n", cus);
+    {  // the global-memory tables of the GL variants: Td3 (= rotl(Td0, 24)) and the byte-replicated InvS
+        constexpr tg::AesTables T;
+        std::vector<uint32_t> h(512);
+        for (int e = 0; e < 256; e++) {
+            const uint32_t v = T.td0[e];
+            h[e] = (v << 24) | (v >> 8);
+            h[256 + e] = (uint32_t)T.inv_sbox[e] * 0x01010101u;
+        }
+        uint32_t* d;
+        (void)hipMalloc(&d, 2048);
+        (void)hipMemcpy(d, h.data(), 2048, hipMemcpyHostToDevice);
+        g_gtab = d;
+    }
     const int lanes = 1024;  // blocks in flight per CU of the reference variant
     std::vector<R> rs;
     rs.push_back(run<1, 0, 16>("product", d_dk, cus, iters, lanes));
@@ -142,10 +190,13 @@ int main(int argc, char** argv) {
     rs.push_back(run<1, 0, 8>("8w", d_dk, cus, iters, lanes));
     rs.push_back(run<1, 0, 16, 1>("product-rot", d_dk, cus, iters, lanes));
     rs.push_back(run<2, 0, 16, 1>("ilp2-rot", d_dk, cus, iters, lanes));
+    rs.push_back(run<1, 0, 16, 1, 1>("rot-glisb", d_dk, cus, iters, lanes));
+    rs.push_back(run<1, 0, 16, 1, 2>("rot-glT3", d_dk, cus, iters, lanes));
     // variants with the same blocks per CU (64 W x ILP lanes' blocks, decrypted the same number
     // of times) must agree word for word: product / keysV / ilp2-8w, and ilp2 / ilp2-keysV
     int bad = 0;
-    if (rs[1].out != rs[0].out || rs[4].out != rs[0].out || rs[6].out != rs[0].out || rs[7].out != rs[2].out) {
+    if (rs[1].out != rs[0].out || rs[4].out != rs[0].out || rs[6].out != rs[0].out || rs[7].out != rs[2].out ||
+        rs[8].out != rs[0].out || rs[9].out != rs[0].out) {
         printf("MISMATCH among the 1024-block variants\n");
         bad = 1;
     }
