@@ -424,11 +424,125 @@ def open_rate(wl, stream, steps):
         status = wl.d_ostatus.download().view(np.int32)
         ok = ok and bool(np.array_equal(status, wl.pt_len.astype(np.int32))) and wl.opened_plaintext_matches()
     t = float(np.median(ms))
-    return {"value": round(wl.plaintext_total / GIB / (t / 1e3), 2), "unit": "GiB/s", "ms": round(t, 4),
-            "roundtrip_exact": ok,
-            "method": "tlsgpu_open_dev over the sealed batch (AES / 3DES: block-parallel CBC decrypt, per-chain "
-                      "padding/seqnum pass, per-record MAC verify; RC4: lane per connection); median of "
-                      "HIP-event-timed calls (RC4/3DES-only batches: variants on two streams, host-timed)"}
+    out = {"value": round(wl.plaintext_total / GIB / (t / 1e3), 2), "unit": "GiB/s", "ms": round(t, 4),
+           "roundtrip_exact": ok,
+           "method": "tlsgpu_open_dev over the sealed batch (AES / 3DES: block-parallel CBC decrypt, per-chain "
+                     "padding/seqnum pass, per-record MAC verify; RC4: lane per connection); median of "
+                     "HIP-event-timed calls (RC4/3DES-only batches: variants on two streams, host-timed)"}
+    if not conc:
+        # batches with AES launches: successive opens through the open pipeline, as the seal's
+        # figure is taken through the seal pipeline; the one-call figure stays beside it
+        pipe_res = open_pipeline_rate(wl, max(2, min(steps, 20)))
+        out = dict(pipe_res, call_value=out["value"], call_ms=out["ms"],
+                   roundtrip_exact=bool(ok and pipe_res["roundtrip_exact"]),
+                   call_method=out["method"])
+    return out
+
+
+def open_pipeline_rate(wl, calls):
+    """The open leg through the open pipeline (tlsgpu_pipeline_open): `calls` successive opens
+    of the sealed batch, each against its own copy of the initial read states -- successive
+    batches of other connections, so every call is a full open -- plaintext arenas rotating
+    between two.  The MAC pass of call k runs beside the decrypt of call k+1.  Two untimed
+    calls first; then wall time from the first timed call to the pipeline's synchronize.
+    Every call's status and both plaintext arenas are checked."""
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import DeviceBuffer, synchronize
+    from tlslite_amd.recordlayer import OpenPipeline
+    calls = max(2, min(int(calls), max(2, int((32 << 30) // max(1, wl.d_states0.nbytes)) - 2)))
+    states = [DeviceBuffer(wl.d_states0.nbytes) for _ in range(calls + 2)]
+    for st in states:
+        N.call("tlsgpu_memcpy_d2d", st.ptr, wl.d_states0.ptr, st.nbytes, None)
+    pts = [wl.d_opt, DeviceBuffer(wl.d_opt.nbytes)]
+    stat = [DeviceBuffer(4 * wl.n_records) for _ in range(calls + 2)]
+    synchronize()
+    with OpenPipeline(wl.n_records) as pipe:
+        def one(k):
+            for var, d_ch, nch in wl.launches:
+                pipe.open(d_ch, nch, wl.d_orecs, wl.n_records, wl.d_wire, pts[k % 2], states[k], stat[k], var)
+        one(calls)
+        one(calls + 1)
+        pipe.synchronize()
+        t0 = time.perf_counter()
+        for k in range(calls):
+            one(k)
+        pipe.synchronize()
+        t = time.perf_counter() - t0
+    want = wl.pt_len.astype(np.int32)
+    ok = all(bool(np.array_equal(s.download().view(np.int32), want)) for s in stat)
+    ok = ok and wl.opened_plaintext_matches()  # pts[0]
+    saved = wl.d_opt
+    wl.d_opt = pts[1]
+    try:
+        ok = ok and wl.opened_plaintext_matches()
+    finally:
+        wl.d_opt = saved
+    for b in states + stat + pts[1:]:
+        b.free()
+    ms = t / calls * 1e3
+    return {"value": round(wl.plaintext_total / GIB / (ms / 1e3), 2), "unit": "GiB/s", "ms": round(ms, 4),
+            "roundtrip_exact": ok, "pipelined_calls": calls,
+            "method": "tlsgpu_pipeline_open: %d successive opens of the sealed batch, each against its own copy of "
+                      "the read states (the MAC pass of call k beside the decrypt of call k+1, two library "
+                      "streams); wall time of the sequence / calls, after 2 untimed calls" % calls}
+
+
+def _leg_ranks(D, res, leg):
+    """Every rank's result of a side leg (rank order), or an error naming the failed ranks."""
+    ranks = [json.loads(b.decode()) for b in D.gather_bytes(json.dumps(res).encode())]
+    bad = [i for i, r in enumerate(ranks) if r is None or "error" in r]
+    return ranks, ({"error": "%s leg failed on rank(s) %s" % (leg, bad), "ranks": ranks} if bad else None)
+
+
+def open_over_ranks(D, res, plaintext_bytes):
+    """The open leg at N > 1: every rank opened its own shard (after a barrier, so at the
+    same time); the job's rate is all ranks' plaintext / the slowest rank's median call time,
+    `roundtrip_exact` the AND over ranks, and each rank's own figure is listed."""
+    ranks, err = _leg_ranks(D, res, "open")
+    total = D.sum(float(plaintext_bytes))
+    if err:
+        return err
+    t = max(float(r["ms"]) for r in ranks)
+    out = dict(ranks[0])
+    out.update({"value": round(total / GIB / (t / 1e3), 2), "ms": round(t, 4),
+                "roundtrip_exact": all(bool(r["roundtrip_exact"]) for r in ranks),
+                "ranks": [{"value": r["value"], "ms": r["ms"], "roundtrip_exact": r["roundtrip_exact"]} for r in ranks],
+                "aggregate": "sum of the ranks' plaintext bytes / the slowest rank's median call time"})
+    return out
+
+
+def derive_over_ranks(D, res):
+    """The derive leg at N > 1: every rank derived its own 4,096 connections at the same time;
+    the job's rate is all ranks' connections / the slowest rank's median call time."""
+    ranks, err = _leg_ranks(D, res, "derive")
+    if err:
+        return err
+    t = max(float(r["ms"]) for r in ranks)
+    n = sum(int(r["connections"]) for r in ranks)
+    out = dict(ranks[0])
+    out.update({"connections": n, "ms": round(t, 4), "conns_per_s": round(n / (t / 1e3)),
+                "key_blocks_exact_sample": all(bool(r["key_blocks_exact_sample"]) for r in ranks),
+                "ranks": [{"ms": r["ms"], "key_blocks_exact_sample": r["key_blocks_exact_sample"]} for r in ranks],
+                "aggregate": "sum of the ranks' connections / the slowest rank's median call time"})
+    return out
+
+
+def host_inclusive_over_ranks(D, res, plaintext_bytes):
+    """The host-inclusive leg at N > 1 (each rank's GPU on its own link): all ranks' plaintext /
+    the slowest rank's best pinned call; bit_exact the AND over ranks and both arena kinds."""
+    ranks, err = _leg_ranks(D, res, "host-inclusive")
+    total = D.sum(float(plaintext_bytes))
+    if err:
+        return err
+    t = max(float(r["pinned"]["ms"]) for r in ranks)
+    out = dict(ranks[0])
+    out.update({"value": round(total / GIB / (t / 1e3), 2),
+                "bit_exact": all(bool(r[k]["bit_exact"]) for r in ranks for k in ("pinned", "pageable")),
+                "ranks": [{"value": r["value"], "pinned_ms": r["pinned"]["ms"],
+                           "bit_exact": bool(r["pinned"]["bit_exact"] and r["pageable"]["bit_exact"])} for r in ranks],
+                "aggregate": "sum of the ranks' plaintext bytes / the slowest rank's best pinned call"})
+    out.pop("pcie_frac", None)
+    return out
 
 
 def derive_rate(stream, nconn=4096, steps=10):
@@ -757,7 +871,8 @@ def main():
     # round trip checked byte-for-byte against the plaintext arena
     progress("open / derive / host-inclusive legs")
     open_res = None
-    if D.world == 1 and args.open:
+    if args.open:
+        D.barrier()  # at N > 1 the ranks open their shards at the same time
         try:
             progress("open leg")
             if args.open_split:
@@ -769,21 +884,29 @@ def main():
                 open_res["split"] = args.open_split
         except Exception as e:  # reported, never silently replaced
             open_res = {"error": str(e)}
+        if D.world > 1:
+            open_res = open_over_ranks(D, open_res, wl.plaintext_total)
 
     derive_res = None
-    if D.world == 1 and args.derive:
+    if args.derive:
+        D.barrier()
         try:
             progress("derive leg")
             derive_res = derive_rate(stream)
         except Exception as e:  # reported, never silently replaced
             derive_res = {"error": str(e)}
+        if D.world > 1:
+            derive_res = derive_over_ranks(D, derive_res)
 
     host_inc = None
-    if D.world == 1 and args.host_inclusive:
+    if args.host_inclusive:
+        D.barrier()
         try:
             host_inc = host_inclusive_rate(wl)
         except Exception as e:  # reported, never silently replaced
             host_inc = {"error": str(e)}
+        if D.world > 1 and D.sum(0.0 if host_inc is None else 1.0) > 0:  # None: a multi-variant batch
+            host_inc = host_inclusive_over_ranks(D, host_inc, wl.plaintext_total)
 
     if D.rank == 0:
         out = {

@@ -85,3 +85,55 @@ def test_pmc_traffic_attached_only_to_the_same_workload(tmp_path):
     for cfg in ("cfg2", "cfg3", "cfg4", "cfg5"):
         pj = json.load(open(os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg)))
         assert pj["workload"].startswith(cfg) and pj["records"] > 0 and pj["hbm_bytes_per_launch"] > 0
+
+
+class _FakeRanks:
+    """Two ranks' results as ShardGroup.gather_bytes / sum would return them on rank 0."""
+
+    def __init__(self, results, nbytes):
+        import json
+        self._b = [json.dumps(r).encode() for r in results]
+        self._n = nbytes
+
+    def gather_bytes(self, b):
+        return self._b
+
+    def sum(self, x):
+        return float(sum(self._n))
+
+
+def test_open_leg_aggregated_over_ranks():
+    """bench.py's open leg at N > 1 (open_over_ranks): the job's rate is all ranks' plaintext /
+    the slowest rank's median call, roundtrip_exact the AND over ranks, a failing rank an
+    error -- never a silently dropped rank."""
+    import bench
+    gib = bench.GIB
+    a = {"value": 800.0, "unit": "GiB/s", "ms": 1.25, "roundtrip_exact": True, "method": "m"}
+    b = {"value": 780.0, "unit": "GiB/s", "ms": 1.30, "roundtrip_exact": True, "method": "m"}
+    r = bench.open_over_ranks(_FakeRanks([a, b], [gib, gib]), a, gib)
+    assert r["value"] == round(2.0 / (1.30 / 1e3), 2) and r["ms"] == 1.3 and r["roundtrip_exact"] is True
+    assert [x["value"] for x in r["ranks"]] == [800.0, 780.0]
+    b2 = dict(b, roundtrip_exact=False)
+    assert bench.open_over_ranks(_FakeRanks([a, b2], [gib, gib]), a, gib)["roundtrip_exact"] is False
+    r = bench.open_over_ranks(_FakeRanks([a, {"error": "boom"}], [gib, gib]), a, gib)
+    assert "error" in r and "rank(s) [1]" in r["error"]
+
+
+def test_derive_and_host_legs_aggregated_over_ranks():
+    """The derive and host-inclusive legs at N > 1 (derive_over_ranks,
+    host_inclusive_over_ranks): sums over ranks / the slowest rank, exactness ANDed."""
+    import bench
+    gib = bench.GIB
+    d0 = {"connections": 4096, "ms": 0.8, "conns_per_s": 5120000, "key_blocks_exact_sample": True}
+    d1 = dict(d0, ms=1.0, key_blocks_exact_sample=False)
+    r = bench.derive_over_ranks(_FakeRanks([d0, d1], [0, 0]), d0)
+    assert r["connections"] == 8192 and r["ms"] == 1.0 and r["conns_per_s"] == 8192000
+    assert r["key_blocks_exact_sample"] is False
+    h = {"value": 40.0, "pinned": {"value": 40.0, "ms": 25.0, "bit_exact": True},
+         "pageable": {"value": 30.0, "ms": 33.0, "bit_exact": True}, "pcie_frac": 0.9}
+    r = bench.host_inclusive_over_ranks(_FakeRanks([h, h], [gib, gib]), h, gib)
+    assert r["value"] == round(2.0 / 0.025, 2) and r["bit_exact"] is True and "pcie_frac" not in r
+    hb = {"value": 40.0, "pinned": {"value": 40.0, "ms": 25.0, "bit_exact": True},
+          "pageable": {"value": 30.0, "ms": 33.0, "bit_exact": False}}
+    assert bench.host_inclusive_over_ranks(_FakeRanks([h, hb], [gib, gib]), h, gib)["bit_exact"] is False
+    assert "error" in bench.host_inclusive_over_ranks(_FakeRanks([h, None], [gib, gib]), h, gib)

@@ -338,3 +338,71 @@ def test_split_open_parts_like_oracle(suite, version, mode):
     assert stopped, "no alerts exercised"
     for r, o in zip(readers, oreaders):
         assert r.seqnum == o.seqnum and r.iv == o.iv
+
+
+@pytest.mark.parametrize("suites,version", [(["AES128-SHA"], (3, 3)), (["AES256-SHA256", "AES128-SHA"], (3, 3)),
+                                            (["3DES-SHA", "RC4-SHA"], (3, 1)), (["AES128-SHA", "RC4-MD5"], (3, 0))])
+def test_open_pipeline_batches_like_oracle(suites, version):
+    """The open pipeline (tlsgpu_pipeline_open via open_batches): 5 successive batches of the
+    same connections -- the MAC pass of batch k beside the decrypt of batch k+1, batch k's
+    stop pass after batch k+1's decrypt.  ~3 % of records tampered or truncated; a
+    connection that alerts in batch k reports ALERT_SKIPPED for its later records in batch k
+    AND in every later batch (ConnState.closed), and its state stays as the failing record
+    left it.  Every status, plaintext and final state equals the oracle's reading the
+    batches in order (tlsrecordlayer.py:958-1044, :1039-1042)."""
+    from oracle import oracle as O
+    from tlslite_amd import _native as N
+    from tlslite_amd.recordlayer import open_batches
+    T = _T()
+    rng = np.random.default_rng(zlib.crc32(repr(("opipe", suites, version)).encode()))
+    amap = {0: 0, O.ALERT_BAD_RECORD_MAC: N.ALERT_BAD_RECORD_MAC,
+            O.ALERT_DECRYPTION_FAILED: N.ALERT_DECRYPTION_FAILED}
+    nconn, nbatch = 500, 5
+    writers, readers, oreaders, suite_of = [], [], [], []
+    for ci in range(nconn):
+        suite = suites[ci % len(suites)]
+        mk_t, mk_o = _mk(T, O, suite, version, rng)
+        writers.append(mk_t())
+        readers.append(mk_t())
+        oreaders.append(mk_o())
+        suite_of.append(suite)
+    batches = []
+    for _ in range(nbatch):
+        plan = []
+        for ci in range(nconn):
+            for _ in range(int(rng.integers(0, 3))):
+                n = int(rng.choice([int(rng.integers(1, 300)), int(rng.integers(300, 16385))]))
+                plan.append((ci, rng.bytes(n), int(rng.choice([21, 22, 23], p=[0.05, 0.05, 0.9]))))
+        wires = T.seal(writers, plan)
+        recs = []
+        for (ci, _, ct), w in zip(plan, wires):
+            body = bytearray(w[5:])
+            u = rng.random()
+            if u < 0.02:
+                body[int(rng.integers(0, len(body)))] ^= 1 << int(rng.integers(0, 8))
+            elif u < 0.03 and O.SUITES[suite_of[ci]][0] != "rc4":
+                body = body[:-1]
+            recs.append((ci, ct, bytes(body)))
+        batches.append(recs)
+    res = open_batches(readers, batches)
+    stopped = set()
+    for recs, out in zip(batches, res):
+        assert len(out) == len(recs)
+        for (ci, ct, body), (st, p) in zip(recs, out):
+            if ci in stopped:
+                assert st == N.ALERT_SKIPPED and p is None
+                continue
+            ost, opt = oreaders[ci].open(body, ct)
+            assert st == amap[ost]
+            if ost == 0:
+                assert p == opt
+            else:
+                assert p is None
+                stopped.add(ci)
+    assert stopped, "no alerts exercised"
+    for ci, (r, o) in enumerate(zip(readers, oreaders)):
+        assert r.seqnum == o.seqnum, ci
+        if O.SUITES[suite_of[ci]][0] == "rc4":
+            assert r.rc4 == o.rc4, ci
+        else:
+            assert r.iv == o.iv, ci

@@ -43,7 +43,11 @@ struct ConnState {
     uint32_t dk[60];       // AES equivalent-inverse-cipher round keys, LE column words
     uint32_t des[3][32];   // 3DES: per key, 16 rounds x {even-box word, odd-box word}
     uint8_t rc4_S[256];    // Python_RC4.S (python_rc4.py:21)
-    uint8_t reserved[TLSGPU_CONN_STATE_BYTES - 1376];
+    uint32_t closed;       // open direction: 1 once a TLSGPU_CHAIN_STOP_ON_ALERT chain of this state hit
+                           // an alert -- the reference closes the connection there (tlsrecordlayer.py:
+                           // 524-529, 1039-1042); every later open of the state reports
+                           // TLSGPU_ALERT_SKIPPED and leaves it unchanged (round 5)
+    uint8_t reserved[TLSGPU_CONN_STATE_BYTES - 1380];
 };
 // Line map (128 B, the HBM request size): line 0 = everything prefix_kernel reads, the
 // chain's CBC residue and fixedIVBlock ([0,64)) and the HMAC midstates ([64,128), mac_kernel);
@@ -52,6 +56,7 @@ static_assert(__builtin_offsetof(ConnState, iv) == 32 && __builtin_offsetof(Conn
               "prefix/cipher fields in the first sector");
 static_assert(__builtin_offsetof(ConnState, mac_in) == 64, "HMAC midstates in the second sector");
 static_assert(__builtin_offsetof(ConnState, ek) == 256, "round keys line-aligned");
+static_assert(__builtin_offsetof(ConnState, closed) == 1376, "closed mark after the RC4 state");
 // the ABI blob (tlsgpu_conn_state) and the device struct must have the same stride
 static_assert(sizeof(ConnState) == TLSGPU_CONN_STATE_BYTES, "ConnState must be exactly 2048 bytes");
 

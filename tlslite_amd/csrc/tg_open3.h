@@ -18,11 +18,12 @@
 //                       computed and so whether a seqnum is consumed (:1018).
 //   open_mac_kernel     one lane per record: MAC over the plaintext, compare
 //                       (:1006-1039), status.
-//   open_stop_kernel    one lane per chain, TLSGPU_CHAIN_STOP_ON_ALERT chains
-//                       only: records after the first alert become
-//                       TLSGPU_ALERT_SKIPPED and the state is rolled back to
-//                       what the failing record left (the reference closes the
-//                       connection at the alert, :1039-1042).
+//   open_stop_kernel    one lane per chain, TLSGPU_CHAIN_STOP_ON_ALERT chains:
+//                       records after the first alert become TLSGPU_ALERT_SKIPPED,
+//                       the state is rolled back to what the failing record left
+//                       and marked closed (the reference closes the connection at
+//                       the alert, :1039-1042); a state closed before the pass has
+//                       every record of its chain skipped.
 //
 // Workspace per record: one 48-byte OpenMeta and one 48-byte OpenMacState.
 //
@@ -137,6 +138,9 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
     }
     const bool ok = sok & (h0.x == (uint32_t)CIPHER_ID) & (h0.y == (uint32_t)MAC) & (h0.w == (SSL3 ? 1u : 0u)) &
                     (h1.w == 0u);
+    // a state closed by an earlier alert (ConnState.closed): every record skipped, nothing
+    // opened, the state untouched
+    const bool closed = ok && st->closed != 0u;
     const uint32_t E = h1.z ? BS : 0u;
     for (uint32_t k = 0; k < ch.count; k++) {
         const uint32_t r = ch.first + k;
@@ -151,8 +155,9 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
         m.len = 0;
         m.n = 0;
         m.chain = cid;
-        if (!ok) {
-            status[r] = sok ? TLSGPU_EMISMATCH : TLSGPU_EINVAL;
+        if (!ok || closed) {
+            status[r] = !sok ? TLSGPU_EINVAL : closed ? TLSGPU_ALERT_SKIPPED : TLSGPU_EMISMATCH;
+            m.epoch = closed ? 0u : m.epoch;  // no later pass of this launch looks at a closed chain's records
         } else {
             const tlsgpu_open_record R = recs[r];
             const uint32_t L = R.ct_len;
@@ -178,7 +183,7 @@ __global__ void __launch_bounds__(256) open_prefix_kernel(const tlsgpu_chain* __
         }
         meta[r] = m;
     }
-    if (ok) {
+    if (ok && !closed) {
 #pragma unroll
         for (int i = 0; i < (int)BS / 4; i++) st->iv[i] = res[i];
     }
@@ -500,6 +505,7 @@ __global__ void __launch_bounds__(256) open_seq_kernel(const tlsgpu_chain* __res
     const tlsgpu_chain ch = chains[cid];
     if (ch.state >= nstates) return;  // refused by open_prefix_kernel (ABI 6): no state read
     ConnState* st = states + ch.state;
+    if (st->closed) return;  // closed by an earlier alert: skipped (open_prefix_kernel), state untouched
     uint64_t seq = st->seqnum;
     bool any = false;
     for (uint32_t k = 0; k < ch.count; k++) {
@@ -618,10 +624,20 @@ __global__ void __launch_bounds__(256) open_stop_kernel(const tlsgpu_chain* __re
                                                        const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
                                                        const uint8_t* __restrict__ wire, ConnState* __restrict__ states,
                                                        int32_t* __restrict__ status,
-                                                       const OpenMeta* __restrict__ meta, uint32_t epoch) {
+                                                       const OpenMeta* __restrict__ meta, uint32_t epoch,
+                                                       uint32_t nstates) {
     const uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
     if (cid >= nchains) return;
     const tlsgpu_chain ch = chains[cid];
+    if (ch.state >= nstates) return;  // refused by open_prefix_kernel (ABI 6)
+    ConnState* st = states + ch.state;
+    if (st->closed) {
+        // closed before this pass: by an earlier call, or -- in an open pipeline, where this
+        // call's decrypt ran before the previous call's stop pass -- by the previous call.
+        // Every record of the chain is skipped; the state stays as the closing alert left it.
+        for (uint32_t k = 0; k < ch.count && ch.first + k < nrecords; k++) status[ch.first + k] = TLSGPU_ALERT_SKIPPED;
+        return;
+    }
     if (!(ch.flags & TLSGPU_CHAIN_STOP_ON_ALERT)) return;
     for (uint32_t k = 0; k < ch.count; k++) {
         const uint32_t r = ch.first + k;
@@ -629,11 +645,13 @@ __global__ void __launch_bounds__(256) open_stop_kernel(const tlsgpu_chain* __re
         const int32_t s = status[r];
         if (s != TLSGPU_ALERT_BAD_RECORD_MAC && s != TLSGPU_ALERT_DECRYPTION_FAILED) continue;
         const OpenMeta& m = meta[r];
-        if (m.epoch != epoch || k + 1 == ch.count) return;
+        if (m.epoch != epoch) return;
+        st->closed = 1u;  // the reference closes the connection at the alert (:524-529, :1039-1042)
         for (uint32_t j = k + 1; j < ch.count && ch.first + j < nrecords; j++) status[ch.first + j] = TLSGPU_ALERT_SKIPPED;
         // state as record r left it: its seqnum was consumed iff its MAC was computed, and its
-        // last ciphertext block is the residue iff it was decrypted (a block multiple)
-        ConnState* st = states + m.state;
+        // last ciphertext block is the residue iff it was decrypted (a block multiple).  Written
+        // even when r is the chain's last record: in an open pipeline the next call's prefix and
+        // padding passes may already have advanced the state (tlsgpu_pipeline_open).
         st->seqnum = m.seq + ((m.flags & OM_VERIFY) ? 1u : 0u);
         const tlsgpu_open_record R = recs[r];
         uint32_t res[4] = {m.pred[0], m.pred[1], m.pred[2], m.pred[3]};

@@ -192,6 +192,40 @@ class SealPipeline:
         self.close()
 
 
+class OpenPipeline:
+    """Overlapped batch open (tlsgpu_open_pipeline_*): successive open() calls -- successive
+    batches of received records -- run the MAC pass of call k beside the decrypt of call
+    k+1 on two library-owned streams.  Each call has the semantics of open_dev (a chain
+    closed by an alert in one call reports TLSGPU_ALERT_SKIPPED for its records in later
+    calls); results are complete after synchronize()."""
+
+    def __init__(self, max_records):
+        h = ctypes.c_void_p()
+        N.call("tlsgpu_open_pipeline_create", ctypes.byref(h), int(max_records))
+        self.handle = h
+        self.max_records = int(max_records)
+
+    def open(self, chains, nchains, records, nrecords, wire, pt, states, status, variant, wire_bytes=None,
+             pt_bytes=None, nstates=None):
+        N.call("tlsgpu_pipeline_open", self.handle, _p(chains), int(nchains), _p(records), int(nrecords), _p(wire),
+               _size(wire, wire_bytes, "wire"), _p(pt), _size(pt, pt_bytes, "pt"), _p(states),
+               _nstates(states, nstates), _p(status), variant)
+
+    def synchronize(self):
+        N.call("tlsgpu_open_pipeline_synchronize", self.handle)
+
+    def close(self):
+        if self.handle is not None and self.handle.value:
+            N.call("tlsgpu_open_pipeline_destroy", self.handle)
+        self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 class HostSealPipeline:
     """Seal batches whose plaintext and wire arenas live in HOST memory
     (tlsgpu_host_pipeline_*): the records' socket-buffer hand-off
@@ -374,59 +408,105 @@ def open_records(states, records, stream=None, stop_on_alert=True):
     nrec = len(records)
     if nrec == 0:
         return []
-    by_state = OrderedDict()
-    for i, r in enumerate(records):
-        by_state.setdefault(r[0], []).append(i)
-    order = [i for idxs in by_state.values() for i in idxs]
-    ct_off = np.zeros(nrec, dtype=np.uint64)
-    pos = 0
-    for k, i in enumerate(order):
-        ct_off[k] = pos
-        pos += len(records[i][2])
-        pos += (-pos) % PT_ALIGN
-    total = max(pos, 16)
-    host = np.zeros(total, dtype=np.uint8)
-    for k, i in enumerate(order):
-        b = bytes(records[i][2])
-        if b:
-            host[int(ct_off[k]):int(ct_off[k]) + len(b)] = np.frombuffer(b, dtype=np.uint8)
-    recs = make_open_records(ct_off, ct_off, [len(records[i][2]) for i in order], [records[i][1] for i in order])
-    buckets = OrderedDict()
-    first = 0
-    for si, idxs in by_state.items():
-        buckets.setdefault(states[si].variant, []).append((si, first, len(idxs)))
-        first += len(idxs)
-    d_ct = DeviceBuffer(total)
-    d_pt = DeviceBuffer(total)
-    d_recs = DeviceBuffer(ctypes.sizeof(recs))
-    d_st = DeviceBuffer(4 * nrec)
     d_states = DeviceBuffer(STATE_BYTES * len(states))
-    d_ct.upload(host, stream=stream)
-    d_recs.upload(np.frombuffer(recs, dtype=np.uint8), stream=stream)
     d_states.upload(pack_states(states), stream=stream)
-    d_pt.zero(stream)
-    keep = []
-    for var, chs in buckets.items():
-        c = make_chains([x[0] for x in chs], [x[1] for x in chs], [x[2] for x in chs],
-                        N.CHAIN_STOP_ON_ALERT if stop_on_alert else 0)
-        d_ch = DeviceBuffer(ctypes.sizeof(c))
-        d_ch.upload(np.frombuffer(c, dtype=np.uint8), stream=stream)
-        keep.append(d_ch)
-        open_dev(d_ch, len(chs), d_recs, nrec, d_ct, d_pt, d_states, d_st, var, stream=stream)
+    b = _OpenBatch(states, records, stream, stop_on_alert)
+    for var, d_ch, nch in b.calls:
+        open_dev(d_ch, nch, b.d_recs, nrec, b.d_ct, b.d_pt, d_states, b.d_st, var, stream=stream)
     if stream is not None:
         stream.synchronize()
-    pt_host = d_pt.download()
-    status = d_st.download().view(np.int32)
+    out = b.results()
     unpack_states(d_states.download(), states)
     synchronize()
-    out = [None] * nrec
-    for k, i in enumerate(order):
-        st = int(status[k])
-        if st < 0:
-            out[i] = (st, None)
-        else:
-            o = int(ct_off[k])
-            out[i] = (0, pt_host[o:o + st].tobytes())
+    return out
+
+
+class _OpenBatch:
+    """One batch of received records staged in device memory for an open: the ciphertext
+    arena (records of one state contiguous, in list order), the plaintext arena, descriptors,
+    status, and one chain list per suite variant (self.calls: (variant, chains, nchains))."""
+
+    def __init__(self, states, records, stream, stop_on_alert):
+        self.nrec = nrec = len(records)
+        by_state = OrderedDict()
+        for i, r in enumerate(records):
+            by_state.setdefault(r[0], []).append(i)
+        self.order = order = [i for idxs in by_state.values() for i in idxs]
+        self.ct_off = ct_off = np.zeros(nrec, dtype=np.uint64)
+        pos = 0
+        for k, i in enumerate(order):
+            ct_off[k] = pos
+            pos += len(records[i][2])
+            pos += (-pos) % PT_ALIGN
+        total = max(pos, 16)
+        host = np.zeros(total, dtype=np.uint8)
+        for k, i in enumerate(order):
+            b = bytes(records[i][2])
+            if b:
+                host[int(ct_off[k]):int(ct_off[k]) + len(b)] = np.frombuffer(b, dtype=np.uint8)
+        recs = make_open_records(ct_off, ct_off, [len(records[i][2]) for i in order],
+                                 [records[i][1] for i in order])
+        buckets = OrderedDict()
+        first = 0
+        for si, idxs in by_state.items():
+            buckets.setdefault(states[si].variant, []).append((si, first, len(idxs)))
+            first += len(idxs)
+        self.d_ct = DeviceBuffer(total)
+        self.d_pt = DeviceBuffer(total)
+        self.d_recs = DeviceBuffer(ctypes.sizeof(recs))
+        self.d_st = DeviceBuffer(4 * nrec)
+        self.d_ct.upload(host, stream=stream)
+        self.d_recs.upload(np.frombuffer(recs, dtype=np.uint8), stream=stream)
+        self.d_pt.zero(stream)
+        self.calls = []
+        for var, chs in buckets.items():
+            c = make_chains([x[0] for x in chs], [x[1] for x in chs], [x[2] for x in chs],
+                            N.CHAIN_STOP_ON_ALERT if stop_on_alert else 0)
+            d_ch = DeviceBuffer(ctypes.sizeof(c))
+            d_ch.upload(np.frombuffer(c, dtype=np.uint8), stream=stream)
+            self.calls.append((var, d_ch, len(chs)))
+
+    def results(self):
+        """[(status, plaintext or None)] in the batch's list order (after the open completed)."""
+        pt_host = self.d_pt.download()
+        status = self.d_st.download().view(np.int32)
+        out = [None] * self.nrec
+        for k, i in enumerate(self.order):
+            st = int(status[k])
+            if st < 0:
+                out[i] = (st, None)
+            else:
+                o = int(self.ct_off[k])
+                out[i] = (0, pt_host[o:o + st].tobytes())
+        return out
+
+
+def open_batches(states, batches, stream=None, stop_on_alert=True):
+    """Open successive batches of received records through the open pipeline (OpenPipeline:
+    the MAC pass of batch k beside the decrypt of batch k+1), the states device-resident
+    throughout -- what open_records on each batch in turn returns, with the connection
+    semantics carried across batches (a connection stopped by an alert in one batch
+    reports N.ALERT_SKIPPED in later ones).  batches: lists as open_records takes them.
+    Returns one result list per batch."""
+    batches = [list(b) for b in batches]
+    d_states = DeviceBuffer(STATE_BYTES * len(states))
+    d_states.upload(pack_states(states), stream=stream)
+    if stream is not None:
+        stream.synchronize()
+    staged = [_OpenBatch(states, recs, stream, stop_on_alert) if recs else None for recs in batches]
+    if stream is not None:
+        stream.synchronize()
+    synchronize()
+    with OpenPipeline(max([len(b) for b in batches] + [1])) as pipe:
+        for b in staged:
+            if b is None:
+                continue
+            for var, d_ch, nch in b.calls:
+                pipe.open(d_ch, nch, b.d_recs, b.nrec, b.d_ct, b.d_pt, d_states, b.d_st, var)
+        pipe.synchronize()
+    out = [b.results() if b is not None else [] for b in staged]
+    unpack_states(d_states.download(), states)
+    synchronize()
     return out
 
 
