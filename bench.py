@@ -429,62 +429,7 @@ def open_rate(wl, stream, steps):
            "method": "tlsgpu_open_dev over the sealed batch (AES / 3DES: block-parallel CBC decrypt, per-chain "
                      "padding/seqnum pass, per-record MAC verify; RC4: lane per connection); median of "
                      "HIP-event-timed calls (RC4/3DES-only batches: variants on two streams, host-timed)"}
-    if not conc:
-        # batches with AES launches: successive opens through the open pipeline, as the seal's
-        # figure is taken through the seal pipeline; the one-call figure stays beside it
-        pipe_res = open_pipeline_rate(wl, max(2, min(steps, 20)))
-        out = dict(pipe_res, call_value=out["value"], call_ms=out["ms"],
-                   roundtrip_exact=bool(ok and pipe_res["roundtrip_exact"]),
-                   call_method=out["method"])
     return out
-
-
-def open_pipeline_rate(wl, calls):
-    """The open leg through the open pipeline (tlsgpu_pipeline_open): `calls` successive opens
-    of the sealed batch, each against its own copy of the initial read states -- successive
-    batches of other connections, so every call is a full open -- plaintext arenas rotating
-    between two.  The MAC pass of call k runs beside the decrypt of call k+1.  Two untimed
-    calls first; then wall time from the first timed call to the pipeline's synchronize.
-    Every call's status and both plaintext arenas are checked."""
-    from tlslite_amd import _native as N
-    from tlslite_amd.device import DeviceBuffer, synchronize
-    from tlslite_amd.recordlayer import OpenPipeline
-    calls = max(2, min(int(calls), max(2, int((32 << 30) // max(1, wl.d_states0.nbytes)) - 2)))
-    states = [DeviceBuffer(wl.d_states0.nbytes) for _ in range(calls + 2)]
-    for st in states:
-        N.call("tlsgpu_memcpy_d2d", st.ptr, wl.d_states0.ptr, st.nbytes, None)
-    pts = [wl.d_opt, DeviceBuffer(wl.d_opt.nbytes)]
-    stat = [DeviceBuffer(4 * wl.n_records) for _ in range(calls + 2)]
-    synchronize()
-    with OpenPipeline(wl.n_records) as pipe:
-        def one(k):
-            for var, d_ch, nch in wl.launches:
-                pipe.open(d_ch, nch, wl.d_orecs, wl.n_records, wl.d_wire, pts[k % 2], states[k], stat[k], var)
-        one(calls)
-        one(calls + 1)
-        pipe.synchronize()
-        t0 = time.perf_counter()
-        for k in range(calls):
-            one(k)
-        pipe.synchronize()
-        t = time.perf_counter() - t0
-    want = wl.pt_len.astype(np.int32)
-    ok = all(bool(np.array_equal(s.download().view(np.int32), want)) for s in stat)
-    ok = ok and wl.opened_plaintext_matches()  # pts[0]
-    saved = wl.d_opt
-    wl.d_opt = pts[1]
-    try:
-        ok = ok and wl.opened_plaintext_matches()
-    finally:
-        wl.d_opt = saved
-    for b in states + stat + pts[1:]:
-        b.free()
-    ms = t / calls * 1e3
-    return {"value": round(wl.plaintext_total / GIB / (ms / 1e3), 2), "unit": "GiB/s", "ms": round(ms, 4),
-            "roundtrip_exact": ok, "pipelined_calls": calls,
-            "method": "tlsgpu_pipeline_open: %d successive opens of the sealed batch, each against its own copy of "
-                      "the read states (the MAC pass of call k beside the decrypt of call k+1, two library "
-                      "streams); wall time of the sequence / calls, after 2 untimed calls" % calls}
 
 
 def _leg_ranks(D, res, leg):

@@ -344,23 +344,6 @@ int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_o
 enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_NONE = 2,
        TLSGPU_OPEN_SPLIT_BLOCKS = 3 };
 int tlsgpu_set_open_parts(int mode, int64_t min_records);
-/* ---- open pipeline (ABI 6, round 5): successive tlsgpu_pipeline_open calls -- successive
- * batches of received records -- overlap the MAC pass of call k with the decrypt of call
- * k+1 (two library-owned streams, two workspaces in rotation).  Call k's stop-on-alert pass
- * runs after call k+1's decrypt: a chain closed by an alert in call k (ConnState's closed
- * mark, set by every open path) has all its records in later calls reported
- * TLSGPU_ALERT_SKIPPED and its state left as the alert left it -- what tlsgpu_open_dev calls
- * in sequence produce.  Inputs must be ready when a call is made and stay valid, and outputs
- * are complete, only after tlsgpu_open_pipeline_synchronize.  Replaces nothing in the
- * reference (tlslite opens one record at a time, tlsrecordlayer.py:958-1044). */
-typedef struct tlsgpu_open_pipeline_s *tlsgpu_open_pipeline;
-int tlsgpu_open_pipeline_create(tlsgpu_open_pipeline *p, uint32_t max_records);
-int tlsgpu_open_pipeline_destroy(tlsgpu_open_pipeline p);
-int tlsgpu_open_pipeline_synchronize(tlsgpu_open_pipeline p);
-int tlsgpu_pipeline_open(tlsgpu_open_pipeline p, const tlsgpu_chain *chains, uint32_t nchains,
-                         const tlsgpu_open_record *records, uint32_t nrecords, const uint8_t *wire,
-                         size_t wire_bytes, uint8_t *pt, size_t pt_bytes, tlsgpu_conn_state *states,
-                         uint32_t nstates, int32_t *status, uint32_t variant);
 /* raw stateful encrypt (decrypt=0) / decrypt (decrypt=1) of spans; one span
  * per state per launch (a state's spans in one launch run in array order). */
 int tlsgpu_cipher_dev(const tlsgpu_span *spans, uint32_t nspans, const uint8_t *in, uint8_t *out,

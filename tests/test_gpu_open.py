@@ -342,19 +342,18 @@ def test_split_open_parts_like_oracle(suite, version, mode):
 
 @pytest.mark.parametrize("suites,version", [(["AES128-SHA"], (3, 3)), (["AES256-SHA256", "AES128-SHA"], (3, 3)),
                                             (["3DES-SHA", "RC4-SHA"], (3, 1)), (["AES128-SHA", "RC4-MD5"], (3, 0))])
-def test_open_pipeline_batches_like_oracle(suites, version):
-    """The open pipeline (tlsgpu_pipeline_open via open_batches): 5 successive batches of the
-    same connections -- the MAC pass of batch k beside the decrypt of batch k+1, batch k's
-    stop pass after batch k+1's decrypt.  ~3 % of records tampered or truncated; a
-    connection that alerts in batch k reports ALERT_SKIPPED for its later records in batch k
-    AND in every later batch (ConnState.closed), and its state stays as the failing record
-    left it.  Every status, plaintext and final state equals the oracle's reading the
+def test_open_batches_closed_connections_like_oracle(suites, version):
+    """Successive batches of the same connections opened with the states device-resident
+    (open_batches: 5 batches, one open_dev call per batch and variant).  ~3 % of records
+    tampered or truncated; a connection that alerts in batch k is closed in its state
+    (ConnState.closed): it reports ALERT_SKIPPED for its later records in batch k AND in
+    every later batch, and its state stays as the failing record left it.  Every status, plaintext and final state equals the oracle's reading the
     batches in order (tlsrecordlayer.py:958-1044, :1039-1042)."""
     from oracle import oracle as O
     from tlslite_amd import _native as N
     from tlslite_amd.recordlayer import open_batches
     T = _T()
-    rng = np.random.default_rng(zlib.crc32(repr(("opipe", suites, version)).encode()))
+    rng = np.random.default_rng(zlib.crc32(repr(("batches", suites, version)).encode()))
     amap = {0: 0, O.ALERT_BAD_RECORD_MAC: N.ALERT_BAD_RECORD_MAC,
             O.ALERT_DECRYPTION_FAILED: N.ALERT_DECRYPTION_FAILED}
     nconn, nbatch = 500, 5

@@ -111,10 +111,6 @@ SIGNATURES = [
     ("tlsgpu_open_workspace_bytes", _sz, [_u32]),
     ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32, _vp, _sz, _vp]),
     ("tlsgpu_set_open_parts", _i, [_i, ctypes.c_int64]),
-    ("tlsgpu_open_pipeline_create", _i, [ctypes.POINTER(_vp), _u32]),
-    ("tlsgpu_open_pipeline_destroy", _i, [_vp]),
-    ("tlsgpu_open_pipeline_synchronize", _i, [_vp]),
-    ("tlsgpu_pipeline_open", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32]),
     ("tlsgpu_cipher_dev", _i, [_vp, _u32, _vp, _vp, _vp, _i, _i, _vp]),
     ("tlsgpu_derive_states_dev", _i, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("tlsgpu_fill_pattern", _i, [_vp, _sz, _u64, _u64, _vp]),

@@ -901,170 +901,6 @@ int tlsgpu_open_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_o
     return 0;
 }
 
-// ---------------------------------------------------------------- open pipeline
-// Successive tlsgpu_pipeline_open calls (round 5).  Call k's front (prefix, decrypt, padding
-// passes) runs on the high-priority stream; its MAC pass on MAC stream k % 2, so the MAC
-// passes of calls k-1 and k run beside each other and beside the front of call k+1 (one MAC
-// pass holds one wave per SIMD on cfg2 and is latency-bound alone: two of them fill the
-// SIMDs better); its stop pass runs on the same MAC stream after call k+2's front (which
-// waits for it in turn), so every state a closing alert rolls back has been advanced by
-// fronts k+1, k+2 at most, and open_stop_kernel's entry check (ConnState.closed) skips those
-// calls' records of the closed chain.  Three workspaces in rotation: call k+3's front waits
-// for call k's stop pass, the last reader of its workspace.
-constexpr int OPIPE_WS = 3;
-struct tlsgpu_open_pipeline_s {
-    int dev;
-    hipStream_t dec_s, mac_s[2];
-    hipEvent_t front_done[OPIPE_WS], stop_done[OPIPE_WS];
-    void* ws[OPIPE_WS];
-    size_t ws_bytes;
-    uint64_t k;
-    struct Pending {  // a call whose stop pass is still to run
-        bool valid = false;
-        const tlsgpu_chain* chains;
-        uint32_t nchains;
-        const tlsgpu_open_record* recs;
-        uint32_t nrecords;
-        const uint8_t* wire;
-        ConnState* states;
-        int32_t* status;
-        uint32_t epoch, nstates;
-    } pend[OPIPE_WS];  // by call index % OPIPE_WS
-};
-
-// the stop pass of call j (pending) on MAC stream j % 2, after `after` (the front the pass
-// must follow) and the previous call's stop pass
-static hipError_t opipe_stop(tlsgpu_open_pipeline p, uint64_t j, hipEvent_t after) {
-    auto& q = p->pend[j % OPIPE_WS];
-    const int w = (int)(j % OPIPE_WS);
-    hipStream_t m = p->mac_s[j % 2];
-    hipError_t e = hipSuccess;
-    if (!q.valid) return e;
-    if (after && (e = hipStreamWaitEvent(m, after, 0)) != hipSuccess) return e;
-    if (j > 0 && (e = hipStreamWaitEvent(m, p->stop_done[(j - 1) % OPIPE_WS], 0)) != hipSuccess) return e;
-    e = launch_open_stop(q.chains, q.nchains, q.recs, q.nrecords, q.wire, q.states, q.status,
-                         static_cast<uint8_t*>(p->ws[w]), q.epoch, q.nstates, m);
-    if (e == hipSuccess) e = hipEventRecord(p->stop_done[w], m);
-    q.valid = false;
-    return e;
-}
-
-int tlsgpu_open_pipeline_create(tlsgpu_open_pipeline* out, uint32_t max_records) {
-    if (!out) return fail(TLSGPU_EINVAL, "null");
-    tlsgpu_open_pipeline p = new tlsgpu_open_pipeline_s();
-    TG_HIP(hipGetDevice(&p->dev));
-    int lo_prio = 0, hi_prio = 0;
-    TG_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
-    // the decrypt fronts at high priority: their CU-filling workgroups (the whole LDS of a CU)
-    // get the CUs first as MAC waves leave; they never share a hardware queue with the MAC
-    // streams (§6)
-    TG_HIP(hipStreamCreateWithPriority(&p->dec_s, hipStreamNonBlocking, CFG_OPIPE_PRIO == 0 ? hi_prio : 0));
-    TG_HIP(hipStreamCreateWithPriority(&p->mac_s[0], hipStreamNonBlocking, CFG_OPIPE_PRIO == 1 ? lo_prio : 0));
-    if (CFG_OPIPE_MACS == 2) TG_HIP(hipStreamCreateWithPriority(&p->mac_s[1], hipStreamNonBlocking, CFG_OPIPE_PRIO == 1 ? lo_prio : 0));
-    else p->mac_s[1] = p->mac_s[0];
-    for (int i = 0; i < OPIPE_WS; i++) {
-        TG_HIP(hipEventCreateWithFlags(&p->front_done[i], hipEventDisableTiming));
-        TG_HIP(hipEventCreateWithFlags(&p->stop_done[i], hipEventDisableTiming));
-    }
-    p->ws_bytes = open_workspace_bytes(max_records ? max_records : 1);
-    for (int i = 0; i < OPIPE_WS; i++) TG_HIP(hipMalloc(&p->ws[i], p->ws_bytes));
-    p->k = 0;
-    *out = p;
-    return 0;
-}
-
-// the stop passes still pending (calls k-2, k-1), in call order, after the last front
-static hipError_t opipe_flush(tlsgpu_open_pipeline p) {
-    if (p->k == 0) return hipSuccess;
-    hipEvent_t last = p->front_done[(p->k - 1) % OPIPE_WS];
-    for (uint64_t j = p->k >= 2 ? p->k - 2 : 0; j < p->k; j++) {
-        hipError_t e = opipe_stop(p, j, last);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
-}
-
-int tlsgpu_open_pipeline_synchronize(tlsgpu_open_pipeline p) {
-    if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
-    hipError_t e = opipe_flush(p);
-    if (e != hipSuccess) return fail_hip(e, "open pipeline stop pass");
-    TG_HIP(hipStreamSynchronize(p->dec_s));
-    for (auto& m : p->mac_s) TG_HIP(hipStreamSynchronize(m));
-    return 0;
-}
-
-int tlsgpu_open_pipeline_destroy(tlsgpu_open_pipeline p) {
-    if (!p) return 0;
-    (void)opipe_flush(p);
-    (void)hipStreamSynchronize(p->dec_s);
-    for (auto& m : p->mac_s) (void)hipStreamSynchronize(m);
-    for (int i = 0; i < OPIPE_WS; i++) {
-        (void)hipFree(p->ws[i]);
-        (void)hipEventDestroy(p->front_done[i]);
-        (void)hipEventDestroy(p->stop_done[i]);
-    }
-    (void)hipStreamDestroy(p->dec_s);
-    (void)hipStreamDestroy(p->mac_s[0]);
-    if (p->mac_s[1] != p->mac_s[0]) (void)hipStreamDestroy(p->mac_s[1]);
-    delete p;
-    return 0;
-}
-
-int tlsgpu_pipeline_open(tlsgpu_open_pipeline p, const tlsgpu_chain* chains, uint32_t nchains,
-                         const tlsgpu_open_record* records, uint32_t nrecords, const uint8_t* wire, size_t wire_bytes,
-                         uint8_t* pt, size_t pt_bytes, tlsgpu_conn_state* states, uint32_t nstates, int32_t* status,
-                         uint32_t variant) {
-    if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
-    if (nchains == 0) return 0;
-    if (!chains || !records || !wire || !pt || !states || !status) return fail(TLSGPU_EINVAL, "null pointer");
-    if (open_workspace_bytes(nrecords) > p->ws_bytes) return fail(TLSGPU_EINVAL, "nrecords > pipeline max_records");
-    const uint64_t k = p->k;
-    const int i = (int)(k % OPIPE_WS);
-    Bounds b;
-    b.pt_cap = pt_bytes;
-    b.wire_cap = wire_bytes;
-    b.nstates = nstates;
-    const uint32_t epoch = next_epoch();
-    // workspace i was last read by call k - 3's stop pass, which also wrote its closing alerts
-    if (k >= (uint64_t)OPIPE_WS) TG_HIP(hipStreamWaitEvent(p->dec_s, p->stop_done[i], 0));
-    bool known = false, back = false;
-    hipError_t e = launch_open_front(variant, chains, nchains, records, nrecords, wire, pt, S(states), status,
-                                     static_cast<uint8_t*>(p->ws[i]), epoch, p->dec_s, &known, &back, b);
-    if (!known) return fail(TLSGPU_EINVAL, "unsupported open variant");
-    if (e != hipSuccess) return fail_hip(e, "open pipeline front");
-    TG_HIP(hipEventRecord(p->front_done[i], p->dec_s));
-    // call k - 2's stop pass, now that the fronts up to this one (which may have advanced the
-    // states it rolls back) are enqueued before it; then this call's MAC pass
-    if (k >= 2 && (e = opipe_stop(p, k - 2, p->front_done[i])) != hipSuccess)
-        return fail_hip(e, "open pipeline stop pass");
-    hipStream_t m = p->mac_s[k % 2];
-    if (back) {
-        TG_HIP(hipStreamWaitEvent(m, p->front_done[i], 0));
-        if ((e = launch_open_mac(variant, records, nrecords, pt, S(states), status, static_cast<uint8_t*>(p->ws[i]),
-                                 epoch, nchains, m)) != hipSuccess)
-            return fail_hip(e, "open pipeline MAC pass");
-        auto& q = p->pend[i];
-        q.valid = true;
-        q.chains = chains;
-        q.nchains = nchains;
-        q.recs = records;
-        q.nrecords = nrecords;
-        q.wire = wire;
-        q.states = S(states);
-        q.status = status;
-        q.epoch = epoch;
-        q.nstates = nstates;
-    } else {
-        // nothing follows this call's front (RC4: the whole open, stop-on-alert included): its
-        // "stop pass" is the front itself.  (A later front waits for the stop passes of the
-        // calls three back: transitively every stop pass precedes the fronts after it.)
-        p->pend[i].valid = false;
-        TG_HIP(hipEventRecord(p->stop_done[i], p->dec_s));
-    }
-    p->k++;
-    return 0;
-}
-
 int tlsgpu_derive_states_dev(const tlsgpu_derive_desc* descs, uint32_t n, tlsgpu_conn_state* write_states,
                              tlsgpu_conn_state* read_states, uint8_t* master_out, uint8_t* key_block_out,
                              int32_t* status, tlsgpu_stream s) {

@@ -30,9 +30,5 @@ constexpr int CFG_PAIR_G1 = 8;
 constexpr int CFG_PAIR_GM = 4;
 // seal pipeline: workspaces in rotation (the MAC stream may run PIPE_WS - 1 calls ahead)
 constexpr int CFG_PIPE_WS = 3;
-// open pipeline: stream priorities (0: decrypt high / MAC normal, 1: decrypt normal / MAC low,
-// 2: all normal) and MAC streams (1 or 2)
-constexpr int CFG_OPIPE_PRIO = 0;
-constexpr int CFG_OPIPE_MACS = 2;
 
 }  // namespace tg

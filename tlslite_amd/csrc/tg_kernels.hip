@@ -866,106 +866,5 @@ hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nc
 }
 
 
-// ---------------------------------------------------------------- open pipeline pieces
-// tlsgpu_pipeline_open (tg_api.hip) runs a call's front -- prefix, one decrypt pass, padding
-// pass -- on one stream and its MAC pass on another beside the NEXT call's front; the stop
-// pass runs after the next call's front (ConnState.closed carries a closing alert to the
-// calls whose front ran before it).  RC4 variants have no back: the whole open is the front.
-template <int NR, int MAC, bool SSL3>
-static hipError_t open_front_t(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* recs,
-                               uint32_t nrecords, const uint8_t* wire, uint8_t* pt, ConnState* states,
-                               int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, const Bounds& b) {
-    constexpr int CID = NR == 10 ? TLSGPU_CIPHER_AES128 : NR == 14 ? TLSGPU_CIPHER_AES256 : TLSGPU_CIPHER_3DES;
-    OpenMeta* meta = reinterpret_cast<OpenMeta*>(ws);
-    hipError_t e = hipMemsetAsync(meta, 0, (size_t)nrecords * sizeof(OpenMeta), s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((open_prefix_kernel<CID, MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains,
-                       nchains, recs, nrecords, wire, states, status, meta, epoch, b.wire_cap, b.pt_cap, b.nstates);
-    constexpr uint32_t WPB = (NR == 0 ? OT_THREADS : O3_THREADS) / 64;
-    uint32_t grid = (nrecords + WPB - 1) / WPB;
-    const uint32_t ncu = cu_count(s);
-    grid = grid > ncu ? ncu : (grid ? grid : 1u);
-    if constexpr (NR == 0) {
-        if ((e = set_lds(open_tdes_kernel, DES_LDS_BYTES, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(open_tdes_kernel, dim3(grid), dim3(OT_THREADS), DES_LDS_BYTES, s, recs, nrecords, wire, pt,
-                           states, meta, epoch, 0u, nchains, -1, 0);
-    } else {
-        if ((e = set_lds(open_aes_kernel<NR>, AES_DEC_LDS_BYTES, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(open_aes_kernel<NR>, dim3(grid), dim3(O3_THREADS), AES_DEC_LDS_BYTES, s, recs, nrecords,
-                           wire, pt, states, meta, epoch, 0u, nchains);
-    }
-    hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains,
-                       recs, nrecords, pt, states, status, meta, epoch, 0u, nchains, b.nstates);
-    return hipGetLastError();
-}
-template <int NR, int MAC, bool SSL3>
-static hipError_t open_mac_t(const tlsgpu_open_record* recs, uint32_t nrecords, uint8_t* pt, ConnState* states,
-                             int32_t* status, uint8_t* ws, uint32_t epoch, uint32_t nchains, hipStream_t s) {
-    constexpr int BS = NR == 0 ? 8 : 16;
-    OpenMeta* meta = reinterpret_cast<OpenMeta*>(ws);
-    OpenMacState* ms = reinterpret_cast<OpenMacState*>(ws + (size_t)nrecords * sizeof(OpenMeta));
-    hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3, BS>), dim3((nrecords + 255) / 256), dim3(256), 0, s, recs, nrecords,
-                       pt, states, status, meta, ms, epoch, 0u, nchains, -1, 0);
-    return hipGetLastError();
-}
-
-hipError_t launch_open_front(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
-                             const tlsgpu_open_record* recs, uint32_t nrecords, const uint8_t* wire, uint8_t* pt,
-                             ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s,
-                             bool* known, bool* back, const Bounds& b) {
-    *known = true;
-    *back = true;
-#define TG_OPEN3(CID, NR, MAC_ID, SSL3)                                                                          \
-    if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3))                                                            \
-        return open_front_t<NR, MAC_ID, SSL3>(chains, nchains, recs, nrecords, wire, pt, states, status, ws, epoch, \
-                                              s, b);
-    TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)
-    TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, false)
-    TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA256, false)
-    TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false)
-    TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)
-    TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)
-    TG_OPEN3(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, false)
-    TG_OPEN3(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, true)
-#undef TG_OPEN3
-    *back = false;
-#define TG_OPEN_RC4(MAC_ID, SSL3)                                      \
-    if (variant == TLSGPU_VARIANT(TLSGPU_CIPHER_RC4, MAC_ID, SSL3)) \
-        return launch_rc4_open<MAC_ID, SSL3>(chains, nchains, recs, nrecords, wire, pt, states, status, s, b);
-    TG_OPEN_RC4(TLSGPU_MAC_SHA1, false)
-    TG_OPEN_RC4(TLSGPU_MAC_MD5, false)
-    TG_OPEN_RC4(TLSGPU_MAC_SHA1, true)
-    TG_OPEN_RC4(TLSGPU_MAC_MD5, true)
-#undef TG_OPEN_RC4
-    *known = false;
-    return hipSuccess;
-}
-
-hipError_t launch_open_mac(uint32_t variant, const tlsgpu_open_record* recs, uint32_t nrecords, uint8_t* pt,
-                           ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, uint32_t nchains,
-                           hipStream_t s) {
-#define TG_OPEN3(CID, NR, MAC_ID, SSL3)               \
-    if (variant == TLSGPU_VARIANT(CID, MAC_ID, SSL3)) \
-        return open_mac_t<NR, MAC_ID, SSL3>(recs, nrecords, pt, states, status, ws, epoch, nchains, s);
-    TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, false)
-    TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, false)
-    TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA256, false)
-    TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA256, false)
-    TG_OPEN3(TLSGPU_CIPHER_AES128, 10, TLSGPU_MAC_SHA1, true)
-    TG_OPEN3(TLSGPU_CIPHER_AES256, 14, TLSGPU_MAC_SHA1, true)
-    TG_OPEN3(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, false)
-    TG_OPEN3(TLSGPU_CIPHER_3DES, 0, TLSGPU_MAC_SHA1, true)
-#undef TG_OPEN3
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_open_stop(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* recs,
-                            uint32_t nrecords, const uint8_t* wire, ConnState* states, int32_t* status, uint8_t* ws,
-                            uint32_t epoch, uint32_t nstates, hipStream_t s) {
-    hipLaunchKernelGGL(open_stop_kernel, dim3((nchains + 255) / 256), dim3(256), 0, s, chains, nchains, recs, nrecords,
-                       wire, states, status, reinterpret_cast<const OpenMeta*>(ws), epoch, nstates);
-    return hipGetLastError();
-}
-
 }  // namespace tg
 

@@ -53,18 +53,6 @@ hipError_t launch_cipher(int cipher, int dec, const tlsgpu_span* spans, uint32_t
                          ConnState* states, hipStream_t s, bool* known);
 size_t open_workspace_bytes(uint32_t nrecords);
 bool open_needs_workspace(uint32_t variant);
-// the open pipeline's pieces (tlsgpu_pipeline_open): *back = false for variants whose open
-// is complete after the front (RC4)
-hipError_t launch_open_front(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
-                             const tlsgpu_open_record* recs, uint32_t nrecords, const uint8_t* wire, uint8_t* pt,
-                             ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s,
-                             bool* known, bool* back, const Bounds& b);
-hipError_t launch_open_mac(uint32_t variant, const tlsgpu_open_record* recs, uint32_t nrecords, uint8_t* pt,
-                           ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, uint32_t nchains,
-                           hipStream_t s);
-hipError_t launch_open_stop(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_open_record* recs,
-                            uint32_t nrecords, const uint8_t* wire, ConnState* states, int32_t* status, uint8_t* ws,
-                            uint32_t epoch, uint32_t nstates, hipStream_t s);
 hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
                        const tlsgpu_open_record* recs, uint32_t nrecords, const uint8_t* wire, uint8_t* pt,
                        ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known,

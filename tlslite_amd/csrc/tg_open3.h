@@ -632,9 +632,8 @@ __global__ void __launch_bounds__(256) open_stop_kernel(const tlsgpu_chain* __re
     if (ch.state >= nstates) return;  // refused by open_prefix_kernel (ABI 6)
     ConnState* st = states + ch.state;
     if (st->closed) {
-        // closed before this pass: by an earlier call, or -- in an open pipeline, where this
-        // call's decrypt ran before the previous call's stop pass -- by the previous call.
-        // Every record of the chain is skipped; the state stays as the closing alert left it.
+        // closed by an earlier call (open_prefix_kernel skipped the chain's records already):
+        // every record of the chain is skipped; the state stays as the closing alert left it.
         for (uint32_t k = 0; k < ch.count && ch.first + k < nrecords; k++) status[ch.first + k] = TLSGPU_ALERT_SKIPPED;
         return;
     }
@@ -650,8 +649,7 @@ __global__ void __launch_bounds__(256) open_stop_kernel(const tlsgpu_chain* __re
         for (uint32_t j = k + 1; j < ch.count && ch.first + j < nrecords; j++) status[ch.first + j] = TLSGPU_ALERT_SKIPPED;
         // state as record r left it: its seqnum was consumed iff its MAC was computed, and its
         // last ciphertext block is the residue iff it was decrypted (a block multiple).  Written
-        // even when r is the chain's last record: in an open pipeline the next call's prefix and
-        // padding passes may already have advanced the state (tlsgpu_pipeline_open).
+        // even when r is the chain's last record (the state then already holds it).
         st->seqnum = m.seq + ((m.flags & OM_VERIFY) ? 1u : 0u);
         const tlsgpu_open_record R = recs[r];
         uint32_t res[4] = {m.pred[0], m.pred[1], m.pred[2], m.pred[3]};

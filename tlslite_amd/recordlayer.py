@@ -192,40 +192,6 @@ class SealPipeline:
         self.close()
 
 
-class OpenPipeline:
-    """Overlapped batch open (tlsgpu_open_pipeline_*): successive open() calls -- successive
-    batches of received records -- run the MAC pass of call k beside the decrypt of call
-    k+1 on two library-owned streams.  Each call has the semantics of open_dev (a chain
-    closed by an alert in one call reports TLSGPU_ALERT_SKIPPED for its records in later
-    calls); results are complete after synchronize()."""
-
-    def __init__(self, max_records):
-        h = ctypes.c_void_p()
-        N.call("tlsgpu_open_pipeline_create", ctypes.byref(h), int(max_records))
-        self.handle = h
-        self.max_records = int(max_records)
-
-    def open(self, chains, nchains, records, nrecords, wire, pt, states, status, variant, wire_bytes=None,
-             pt_bytes=None, nstates=None):
-        N.call("tlsgpu_pipeline_open", self.handle, _p(chains), int(nchains), _p(records), int(nrecords), _p(wire),
-               _size(wire, wire_bytes, "wire"), _p(pt), _size(pt, pt_bytes, "pt"), _p(states),
-               _nstates(states, nstates), _p(status), variant)
-
-    def synchronize(self):
-        N.call("tlsgpu_open_pipeline_synchronize", self.handle)
-
-    def close(self):
-        if self.handle is not None and self.handle.value:
-            N.call("tlsgpu_open_pipeline_destroy", self.handle)
-        self.handle = None
-
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *exc):
-        self.close()
-
-
 class HostSealPipeline:
     """Seal batches whose plaintext and wire arenas live in HOST memory
     (tlsgpu_host_pipeline_*): the records' socket-buffer hand-off
@@ -482,28 +448,24 @@ class _OpenBatch:
 
 
 def open_batches(states, batches, stream=None, stop_on_alert=True):
-    """Open successive batches of received records through the open pipeline (OpenPipeline:
-    the MAC pass of batch k beside the decrypt of batch k+1), the states device-resident
-    throughout -- what open_records on each batch in turn returns, with the connection
-    semantics carried across batches (a connection stopped by an alert in one batch
-    reports N.ALERT_SKIPPED in later ones).  batches: lists as open_records takes them.
-    Returns one result list per batch."""
+    """Open successive batches of received records with the states device-resident
+    throughout (one open_dev call per batch and suite variant, in order on one stream) --
+    what open_records on each batch in turn returns, with the connection semantics carried
+    across batches: a connection stopped by an alert in one batch is closed in its state
+    (ConnState.closed) and reports N.ALERT_SKIPPED in later ones.  batches: lists as
+    open_records takes them.  Returns one result list per batch."""
     batches = [list(b) for b in batches]
     d_states = DeviceBuffer(STATE_BYTES * len(states))
     d_states.upload(pack_states(states), stream=stream)
-    if stream is not None:
-        stream.synchronize()
-    staged = [_OpenBatch(states, recs, stream, stop_on_alert) if recs else None for recs in batches]
-    if stream is not None:
-        stream.synchronize()
-    synchronize()
-    with OpenPipeline(max([len(b) for b in batches] + [1])) as pipe:
-        for b in staged:
-            if b is None:
-                continue
+    staged = []
+    for recs in batches:
+        b = _OpenBatch(states, recs, stream, stop_on_alert) if recs else None
+        if b is not None:
             for var, d_ch, nch in b.calls:
-                pipe.open(d_ch, nch, b.d_recs, b.nrec, b.d_ct, b.d_pt, d_states, b.d_st, var)
-        pipe.synchronize()
+                open_dev(d_ch, nch, b.d_recs, b.nrec, b.d_ct, b.d_pt, d_states, b.d_st, var, stream=stream)
+        staged.append(b)
+    if stream is not None:
+        stream.synchronize()
     out = [b.results() if b is not None else [] for b in staged]
     unpack_states(d_states.download(), states)
     synchronize()

@@ -38,13 +38,6 @@
 #define TG_AB_PIPE_WS 3
 #endif
 
-#ifndef TG_AB_OPIPE_PRIO
-#define TG_AB_OPIPE_PRIO 0
-#endif
-#ifndef TG_AB_OPIPE_MACS
-#define TG_AB_OPIPE_MACS 2
-#endif
-
 namespace tg {
 constexpr int CFG_CBC_WAVES = TG_AB_CBC_WAVES;
 constexpr int CFG_MAC_PRIO = TG_AB_MAC_PRIO;
@@ -57,6 +50,4 @@ constexpr int CFG_PAIR_WAVES_MANY = TG_AB_PAIR_WM;
 constexpr int CFG_PAIR_G1 = TG_AB_PAIR_G1;
 constexpr int CFG_PAIR_GM = TG_AB_PAIR_GM;
 constexpr int CFG_PIPE_WS = TG_AB_PIPE_WS;
-constexpr int CFG_OPIPE_PRIO = TG_AB_OPIPE_PRIO;
-constexpr int CFG_OPIPE_MACS = TG_AB_OPIPE_MACS;
 }  // namespace tg
