@@ -82,13 +82,18 @@ enum {
     TLSGPU_ENODEV = -3,     /* no GPU / bad device ordinal */
     TLSGPU_ETOOBIG = -4,    /* record body would not fit the 16-bit length (codec.py:19-20) */
     TLSGPU_EMISMATCH = -5,  /* connection state does not match the launch variant */
+    TLSGPU_EFRAME = -6,     /* received bytes are not a TLS record header: the first byte is no
+                             * content type (tlsrecordlayer.py:850-857 raises SyntaxError) */
     /* open-path per-record status (alerts, tlsrecordlayer.py:964-1042) */
     TLSGPU_ALERT_BAD_RECORD_MAC = -20,
     TLSGPU_ALERT_DECRYPTION_FAILED = -21,
     /* open with TLSGPU_CHAIN_STOP_ON_ALERT: not opened, an earlier record of the
      * chain raised an alert (the reference sends the alert and closes the
      * connection there: tlsrecordlayer.py:1039-1042 -> _sendError) */
-    TLSGPU_ALERT_SKIPPED = -22
+    TLSGPU_ALERT_SKIPPED = -22,
+    /* receive framing: a header announced more than 18432 body bytes (record_overflow,
+     * tlsrecordlayer.py:871-873) */
+    TLSGPU_ALERT_RECORD_OVERFLOW = -23
 };
 
 /* Launch variant = one (cipher, MAC, SSL3-or-TLS) kernel instantiation.
@@ -344,6 +349,26 @@ int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_o
 enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_NONE = 2,
        TLSGPU_OPEN_SPLIT_BLOCKS = 3 };
 int tlsgpu_set_open_parts(int mode, int64_t min_records);
+/* ---- receive framing on the device (ABI 6, round 5): _getNextRecord's header parse
+ * (tlsrecordlayer.py:832-876; RecordHeader3.parse, messages.py:44-49) for n connections'
+ * received bytes in one arena of stream_bytes, connection i's at [conns[i].off, conns[i].off +
+ * conns[i].len).  Each complete record becomes one tlsgpu_open_record {ct_off = pt_off = its
+ * body's offset in the arena, ct_len, content_type}, in connection order from records[0];
+ * chains[i] = {conns[i].state, first, count, chain_flags}; consumed[i] = the bytes of the
+ * connection's framed records (an incomplete trailing record stays for the next call);
+ * status[i] = the number of records framed, or TLSGPU_ALERT_RECORD_OVERFLOW (a header
+ * announcing more than 18432 body bytes: the records before it are framed, the connection
+ * stops there), TLSGPU_EFRAME (a record starting with a byte that is no content type 20-23;
+ * SSLv2 headers belong to the handshake, which is out of scope), TLSGPU_EINVAL (the span
+ * leaves the arena).  Records past max_records are not framed (consumed[] stops before
+ * them).  total (device, one uint32) = records framed.  The result feeds tlsgpu_open_dev
+ * directly (nrecords = max_records, or *total read back), with a plaintext arena of
+ * stream_bytes.  Everything is device memory; workspace: tlsgpu_frame_workspace_bytes(n). */
+size_t tlsgpu_frame_workspace_bytes(uint32_t n);
+int tlsgpu_frame_dev(const uint8_t *stream, size_t stream_bytes, const tlsgpu_span *conns, uint32_t n,
+                     tlsgpu_open_record *records, uint32_t max_records, tlsgpu_chain *chains,
+                     uint32_t chain_flags, uint32_t *consumed, int32_t *status, uint32_t *total,
+                     void *workspace, size_t workspace_bytes, tlsgpu_stream s);
 /* raw stateful encrypt (decrypt=0) / decrypt (decrypt=1) of spans; one span
  * per state per launch (a state's spans in one launch run in array order). */
 int tlsgpu_cipher_dev(const tlsgpu_span *spans, uint32_t nspans, const uint8_t *in, uint8_t *out,

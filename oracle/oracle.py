@@ -19,6 +19,8 @@ MAC = {"sha1": 1, "sha256": 2, "md5": 3}
 FAULT = {None: 0, "badMAC": 1, "badPadding": 2}
 ALERT_BAD_RECORD_MAC = -20
 ALERT_DECRYPTION_FAILED = -21
+ALERT_RECORD_OVERFLOW = -23
+EFRAME = -6
 
 # suite name -> (cipher, key len, iv len, mac, mac len); tlsrecordlayer.py:1063-1095
 SUITES = {
@@ -226,3 +228,29 @@ def seal_batch(protos, chain_begin, chain_count, pt, pt_off, pt_len, wire, wire_
         for i, c in enumerate(protos):
             ctypes.memmove(c.buf, ctypes.addressof(arr) + i * sz, sz)
     return wl
+
+
+def frame(data):
+    """_getNextRecord's record framing over one connection's received bytes
+    (tlsrecordlayer.py:832-876; RecordHeader3.parse, messages.py:44-49), pure Python: every
+    complete record as (content_type, (major, minor), body), stopping at an incomplete record
+    (left for the next read), at a first header byte that is no content type (:850-857 --
+    SyntaxError as soon as that byte arrives; SSLv2 headers are handshake-only and not
+    framed here), or at a header announcing more than 18432 body bytes (:871-873,
+    record_overflow).  Returns (records, consumed, code): code 0, EFRAME or
+    ALERT_RECORD_OVERFLOW."""
+    data = bytes(data)
+    out, pos = [], 0
+    while pos < len(data):
+        if data[pos] not in (20, 21, 22, 23):  # ContentType.all
+            return out, pos, EFRAME
+        if len(data) - pos < 5:
+            break
+        length = (data[pos + 3] << 8) | data[pos + 4]
+        if length > 18432:
+            return out, pos, ALERT_RECORD_OVERFLOW
+        if len(data) - pos - 5 < length:
+            break
+        out.append((data[pos], (data[pos + 1], data[pos + 2]), data[pos + 5:pos + 5 + length]))
+        pos += 5 + length
+    return out, pos, 0

@@ -16,7 +16,7 @@ LIB = os.path.join(LIBDIR, "libtlsgpu.so")
 ARCH = os.environ.get("TLSGPU_ARCH", "gfx950")
 
 SOURCES = ["tg_kernels.hip", "tg_api.hip"]
-HEADERS = ["tg_config.h", "tg_common.h", "tg_hash.h", "tg_device.h", "tg_quad.h", "tg_aes3.h", "tg_open3.h", "tg_launch.h", "tg_keysched.h", "tg_derive.h"]
+HEADERS = ["tg_config.h", "tg_common.h", "tg_hash.h", "tg_device.h", "tg_quad.h", "tg_aes3.h", "tg_open3.h", "tg_frame.h", "tg_launch.h", "tg_keysched.h", "tg_derive.h"]
 
 
 def _hipcc():

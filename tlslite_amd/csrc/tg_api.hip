@@ -901,6 +901,23 @@ int tlsgpu_open_dev(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_o
     return 0;
 }
 
+size_t tlsgpu_frame_workspace_bytes(uint32_t n) { return frame_workspace_bytes(n); }
+
+int tlsgpu_frame_dev(const uint8_t* stream, size_t stream_bytes, const tlsgpu_span* conns, uint32_t n,
+                     tlsgpu_open_record* records, uint32_t max_records, tlsgpu_chain* chains, uint32_t chain_flags,
+                     uint32_t* consumed, int32_t* status, uint32_t* total, void* workspace, size_t workspace_bytes,
+                     tlsgpu_stream s) {
+    if (n == 0) return 0;
+    if (!stream || !conns || !chains || !consumed || !status || !total || !workspace || (!records && max_records))
+        return fail(TLSGPU_EINVAL, "null pointer");
+    if (n > (1u << 26)) return fail(TLSGPU_EINVAL, "too many connections");
+    if (workspace_bytes < frame_workspace_bytes(n)) return fail(TLSGPU_EINVAL, "workspace too small");
+    hipError_t e = launch_frame(stream, stream_bytes, conns, n, records, max_records, chains, chain_flags, consumed,
+                                status, total, static_cast<uint8_t*>(workspace), HS(s));
+    if (e != hipSuccess) return fail_hip(e, "frame launch");
+    return 0;
+}
+
 int tlsgpu_derive_states_dev(const tlsgpu_derive_desc* descs, uint32_t n, tlsgpu_conn_state* write_states,
                              tlsgpu_conn_state* read_states, uint8_t* master_out, uint8_t* key_block_out,
                              int32_t* status, tlsgpu_stream s) {

@@ -53,6 +53,11 @@ hipError_t launch_cipher(int cipher, int dec, const tlsgpu_span* spans, uint32_t
                          ConnState* states, hipStream_t s, bool* known);
 size_t open_workspace_bytes(uint32_t nrecords);
 bool open_needs_workspace(uint32_t variant);
+// receive framing (tg_frame.h)
+size_t frame_workspace_bytes(uint32_t n);
+hipError_t launch_frame(const uint8_t* stream, uint64_t cap, const tlsgpu_span* conns, uint32_t n,
+                        tlsgpu_open_record* recs, uint32_t max_records, tlsgpu_chain* chains, uint32_t chain_flags,
+                        uint32_t* consumed, int32_t* status, uint32_t* total, uint8_t* ws, hipStream_t s);
 hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nchains,
                        const tlsgpu_open_record* recs, uint32_t nrecords, const uint8_t* wire, uint8_t* pt,
                        ConnState* states, int32_t* status, uint8_t* ws, uint32_t epoch, hipStream_t s, bool* known,

@@ -28,6 +28,11 @@ class RecordOverflow(ValueError):
     """A record header announced more than 18432 body bytes (record_overflow)."""
 
 
+class RecordSyntaxError(SyntaxError):
+    """Received bytes do not start a TLS record: the first header byte is no content type
+    (tlsrecordlayer.py:850-857 raises SyntaxError)."""
+
+
 class BadRecordMAC(ValueError):
     """bad_record_mac alert (tlsrecordlayer.py:1039-1042)."""
 
@@ -44,7 +49,11 @@ def parse_records(data):
     out = []
     pos = 0
     data = bytes(data)
-    while len(data) - pos >= 5:
+    while pos < len(data):
+        if data[pos] not in (20, 21, 22, 23):  # ContentType.all, checked as the byte arrives
+            raise RecordSyntaxError("record type byte %d" % data[pos])
+        if len(data) - pos < 5:
+            break
         ctype, vmaj, vmin = data[pos], data[pos + 1], data[pos + 2]
         length = (data[pos + 3] << 8) | data[pos + 4]
         if length > MAX_RECORD_BODY:
@@ -470,6 +479,69 @@ def open_batches(states, batches, stream=None, stop_on_alert=True):
     unpack_states(d_states.download(), states)
     synchronize()
     return out
+
+
+def frame_workspace_bytes(n):
+    return int(N.lib.tlsgpu_frame_workspace_bytes(int(n)))
+
+
+def frame_dev(stream, conns, n, records, max_records, chains, consumed, status, total, workspace=None,
+              chain_flags=None, s=None, stream_bytes=None):
+    """Receive framing on the device (tlsgpu_frame_dev): n connections' received bytes in the
+    `stream` arena (conns: tlsgpu_span {off, len, state} per connection) -> open descriptors
+    (records, from 0, in connection order), one chain per connection, consumed bytes and a
+    status per connection, the record total in `total` (one uint32).  All DeviceBuffers;
+    workspace None: a temporary one."""
+    ws = workspace if workspace is not None else DeviceBuffer(max(16, frame_workspace_bytes(n)))
+    flags = N.CHAIN_STOP_ON_ALERT if chain_flags is None else int(chain_flags)
+    N.call("tlsgpu_frame_dev", _p(stream), _size(stream, stream_bytes, "stream"), _p(conns), int(n), _p(records),
+           int(max_records), _p(chains), flags, _p(consumed), _p(status), _p(total), _p(ws), ws.nbytes,
+           s.handle if s is not None else None)
+    return ws
+
+
+def frame_streams(streams, max_records=None):
+    """Frame each connection's received bytes on the GPU (frame_dev) and bring the result back:
+    one (status, consumed, [(content_type, body bytes), ...]) per connection.  Test / host
+    convenience: the device-resident path feeds frame_dev's descriptors to open_dev."""
+    n = len(streams)
+    offs, pos = [], 0
+    for b in streams:
+        offs.append(pos)
+        pos += len(b)
+        pos += (-pos) % PT_ALIGN
+    arena = np.zeros(max(pos, 16), dtype=np.uint8)
+    for o, b in zip(offs, streams):
+        if b:
+            arena[o:o + len(b)] = np.frombuffer(bytes(b), dtype=np.uint8)
+    spans = (N.Span * n)()
+    a = np.frombuffer(spans, dtype=np.uint8).reshape(n, 16)
+    a[:, 0:8] = np.asarray(offs, dtype=np.uint64).reshape(n, 1).view(np.uint8)
+    a[:, 8:12] = np.asarray([len(b) for b in streams], dtype=np.uint32).reshape(n, 1).view(np.uint8)
+    a[:, 12:16] = np.arange(n, dtype=np.uint32).reshape(n, 1).view(np.uint8)
+    maxr = sum(len(b) // 5 + 1 for b in streams) if max_records is None else int(max_records)
+    d_s, d_sp = DeviceBuffer(arena.nbytes), DeviceBuffer(ctypes.sizeof(spans))
+    d_s.upload(arena)
+    d_sp.upload(np.frombuffer(spans, dtype=np.uint8))
+    d_r = DeviceBuffer(max(1, maxr) * ctypes.sizeof(N.OpenRecord))
+    d_c, d_cons, d_st, d_tot = (DeviceBuffer(16 * n), DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(16))
+    frame_dev(d_s, d_sp, n, d_r, maxr, d_c, d_cons, d_st, d_tot)
+    synchronize()
+    total = int(d_tot.download()[:4].view(np.uint32)[0])
+    recs = np.frombuffer(d_r.download(), dtype=np.uint8).reshape(-1, ctypes.sizeof(N.OpenRecord))
+    ch = d_c.download().view(np.uint32).reshape(n, 4)
+    cons = d_cons.download().view(np.uint32)
+    st = d_st.download().view(np.int32)
+    out = []
+    for i in range(n):
+        first, count = int(ch[i, 1]), int(ch[i, 2])
+        rs = []
+        for r in recs[first:first + count]:
+            off = int(r[0:8].view(np.uint64)[0])
+            ln = int(r[16:20].view(np.uint32)[0])
+            rs.append((int(r[20]), arena[off:off + ln].tobytes()))
+        out.append((int(st[i]), int(cons[i]), rs))
+    return out, total
 
 
 def open_stream(state, data):
