@@ -432,6 +432,69 @@ def open_rate(wl, stream, steps):
     return out
 
 
+def frame_rate(wl, stream, steps):
+    """Receive framing on the device (tlsgpu_frame_dev) for a batch of one-record connections
+    (cfg2 / cfg3 shapes): each connection's received bytes are its wire record (header +
+    body) in the sealed wire arena.  The framed descriptors must equal the batch's own (body
+    offset, length, content type; one chain per connection); then the same batch is opened
+    from them (status = every record's plaintext length).  Median of HIP-event-timed frame
+    calls, and of frame + open calls.  None for other shapes."""
+    import ctypes
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import DeviceBuffer, Event
+    from tlslite_amd.recordlayer import frame_dev, frame_workspace_bytes, open_dev
+    if len(wl.launches) != 1 or not bool((wl.chain_count == 1).all()):
+        return None
+    var, _, nch = wl.launches[0]
+    n = wl.n_chains
+    first = wl.chain_first.astype(np.int64)
+    spans = np.zeros((n, 2), dtype=np.uint64)
+    spans[:, 0] = wl.wire_off[first]
+    sp32 = spans.view(np.uint32).reshape(n, 4)
+    sp32[:, 2] = wl.wire_len[first].astype(np.uint32)
+    sp32[:, 3] = np.arange(n, dtype=np.uint32)
+    d_sp = DeviceBuffer(spans.nbytes)
+    d_sp.upload(spans.view(np.uint8).reshape(-1))
+    d_r = DeviceBuffer(n * ctypes.sizeof(N.OpenRecord))
+    d_c, d_cons, d_st, d_tot = DeviceBuffer(16 * n), DeviceBuffer(4 * n), DeviceBuffer(4 * n), DeviceBuffer(16)
+    ws = DeviceBuffer(frame_workspace_bytes(n))
+    d_ost, d_ows = DeviceBuffer(4 * n), DeviceBuffer(wl.d_ows[0].nbytes)
+    fms, foms = [], []
+    for it in range(max(2, min(steps, 20)) + 1):
+        a, b, c = Event(), Event(), Event()
+        N.call("tlsgpu_memcpy_d2d", wl.d_ostates.ptr, wl.d_states0.ptr, wl.d_ostates.nbytes, stream.handle)
+        a.record(stream)
+        frame_dev(wl.d_wire, d_sp, n, d_r, n, d_c, d_cons, d_st, d_tot, workspace=ws, s=stream)
+        b.record(stream)
+        open_dev(d_c, n, d_r, n, wl.d_wire, wl.d_opt, wl.d_ostates, d_ost, var, d_ows, stream)
+        c.record(stream)
+        stream.synchronize()
+        if it:
+            fms.append(a.elapsed_ms(b))
+            foms.append(a.elapsed_ms(c))
+    recs = np.frombuffer(d_r.download(), dtype=np.uint8).reshape(n, ctypes.sizeof(N.OpenRecord))
+    ct_off = recs[:, 0:8].copy().view(np.uint64).ravel()
+    ct_len = recs[:, 16:20].copy().view(np.uint32).ravel()
+    ch = d_c.download().view(np.uint32).reshape(n, 4)
+    exact = (int(d_tot.download()[:4].view(np.uint32)[0]) == n
+             and bool(np.array_equal(d_st.download().view(np.int32), np.ones(n, dtype=np.int32)))
+             and bool(np.array_equal(ct_off, (wl.wire_off[first] + 5).astype(np.uint64)))
+             and bool(np.array_equal(ct_len, (wl.wire_len[first] - 5).astype(np.uint32)))
+             and bool(np.array_equal(recs[:, 20], wl.rec_ctype[first].astype(np.uint8) if np.ndim(wl.rec_ctype)
+                                     else np.full(n, wl.rec_ctype, dtype=np.uint8)))
+             and bool(np.array_equal(ch[:, 1], np.arange(n, dtype=np.uint32)))
+             and bool(np.array_equal(ch[:, 2], np.ones(n, dtype=np.uint32))))
+    opened = bool(np.array_equal(d_ost.download().view(np.int32), wl.pt_len[first].astype(np.int32)))
+    for buf in (d_sp, d_r, d_c, d_cons, d_st, d_tot, ws, d_ost, d_ows):
+        buf.free()
+    tf, tfo = float(np.median(fms)), float(np.median(foms))
+    return {"records": n, "ms": round(tf, 4), "records_per_s": round(n / (tf / 1e3)),
+            "frame_exact": exact, "open_from_frames_ms": round(tfo, 4),
+            "open_from_frames_value": round(wl.plaintext_total / GIB / (tfo / 1e3), 2), "open_from_frames_exact": opened,
+            "method": "tlsgpu_frame_dev over each connection's received record in the sealed wire arena, then "
+                      "tlsgpu_open_dev on the framed descriptors; medians of HIP-event-timed calls"}
+
+
 def _leg_ranks(D, res, leg):
     """Every rank's result of a side leg (rank order), or an error naming the failed ranks."""
     ranks = [json.loads(b.decode()) for b in D.gather_bytes(json.dumps(res).encode())]
@@ -827,6 +890,9 @@ def main():
             open_res = open_rate(wl, stream, args.steps)
             if args.open_split:
                 open_res["split"] = args.open_split
+            fr = frame_rate(wl, stream, args.steps)
+            if fr is not None:
+                open_res["frame"] = fr
         except Exception as e:  # reported, never silently replaced
             open_res = {"error": str(e)}
         if D.world > 1:
