@@ -18,6 +18,9 @@
  *                              write path of :538-620 (seal + the socket-buffer
  *                              hand-off) with the PCIe copies overlapped
  *   tlsgpu_open_dev .......... tlsrecordlayer.py:958-1044 (_decryptRecord)
+ *   tlsgpu_frame_dev ......... tlsrecordlayer.py:832-876 (_getNextRecord's header
+ *                              parse; RecordHeader3.parse, messages.py:44-49),
+ *                              batched over connections' received bytes
  *   tlsgpu_cipher_dev ........ utils/python_aes.py:20-69, utils/python_rc4.py:25-41,
  *                              utils/openssl_tripledes.py:29-47 (the stateful
  *                              cipher-object encrypt/decrypt behind
@@ -127,8 +130,11 @@ typedef struct tlsgpu_record {
  * Independent chains run in parallel; a record must belong to exactly one
  * chain. */
 #define TLSGPU_CHAIN_STOP_ON_ALERT 1u /* open: records after the first alert are not
-                                         opened (status TLSGPU_ALERT_SKIPPED) and the
-                                         state stays as the failing record left it */
+                                         opened (status TLSGPU_ALERT_SKIPPED), the state
+                                         stays as the failing record left it and is marked
+                                         closed: every later open of that state reports
+                                         TLSGPU_ALERT_SKIPPED (round 5; state init clears
+                                         the mark) */
 typedef struct tlsgpu_chain {
     uint32_t state;    /* index into the states array */
     uint32_t first;    /* first record index */
