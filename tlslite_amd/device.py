@@ -42,9 +42,11 @@ def arch(ordinal=0):
 
 
 class Stream:
-    """A HIP stream of the library (tlsgpu_stream_create); high=True / False: created at
-    high / normal priority (tlsgpu_stream_create_priority) -- two streams whose kernels must
-    overlap are only certain to get separate hardware queues at different priorities."""
+    """A HIP stream of the library (tlsgpu_stream_create, the runtime's normal priority);
+    high=True / False: created at the runtime's greatest / least priority level
+    (tlsgpu_stream_create_priority; the least level is below normal) -- two streams whose
+    kernels must overlap are only certain to get separate hardware queues at different
+    priorities."""
     def __init__(self, default=False, high=None):
         self.handle = ctypes.c_void_p(None)
         self._own = not default
