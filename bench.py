@@ -432,6 +432,51 @@ def open_rate(wl, stream, steps):
     return out
 
 
+def open_concurrent_rate(wl, calls, nstreams=2):
+    """Successive independent open calls (each against its own copy of the initial read
+    states: batches of different connections) issued round-robin on `nstreams` streams of
+    different priorities, so one call's MAC pass can run beside the next call's decrypt;
+    wall time from the first call to the last stream's synchronize.  Every call's status and
+    each stream's plaintext arena are checked."""
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import DeviceBuffer, Stream, synchronize
+    from tlslite_amd.recordlayer import open_dev, open_workspace_bytes
+    calls = max(nstreams, min(int(calls), max(nstreams, int((24 << 30) // max(1, wl.d_states0.nbytes)))))
+    streams = [Stream(high=(i == 0)) for i in range(nstreams)]
+    states = [DeviceBuffer(wl.d_states0.nbytes) for _ in range(calls)]
+    for st in states:
+        N.call("tlsgpu_memcpy_d2d", st.ptr, wl.d_states0.ptr, st.nbytes, None)
+    pts = [wl.d_opt] + [DeviceBuffer(wl.d_opt.nbytes) for _ in range(nstreams - 1)]
+    wss = [[DeviceBuffer(max(open_workspace_bytes(wl.n_records), 16)) for _ in wl.launches] for _ in range(nstreams)]
+    stat = [DeviceBuffer(4 * wl.n_records) for _ in range(calls)]
+    synchronize()
+
+    def one(k, st):
+        i = k % nstreams
+        for j, (var, d_ch, nch) in enumerate(wl.launches):
+            open_dev(d_ch, nch, wl.d_orecs, wl.n_records, wl.d_wire, pts[i], st, stat[k], var, wss[i][j], streams[i])
+    t0 = time.perf_counter()
+    for k in range(calls):
+        one(k, states[k])
+    for s_ in streams:
+        s_.synchronize()
+    t = time.perf_counter() - t0
+    want = wl.pt_len.astype(np.int32)
+    ok = all(bool(np.array_equal(x.download().view(np.int32), want)) for x in stat)
+    saved = wl.d_opt
+    try:
+        for p_ in pts:
+            wl.d_opt = p_
+            ok = ok and wl.opened_plaintext_matches()
+    finally:
+        wl.d_opt = saved
+    for b in states + stat + pts[1:] + [w for ws in wss for w in ws]:
+        b.free()
+    ms = t / calls * 1e3
+    return {"value": round(wl.plaintext_total / GIB / (ms / 1e3), 2), "ms": round(ms, 4), "calls": calls,
+            "streams": nstreams, "roundtrip_exact": ok}
+
+
 def frame_rate(wl, stream, steps):
     """Receive framing on the device (tlsgpu_frame_dev) for a batch of one-record connections
     (cfg2 / cfg3 shapes): each connection's received bytes are its wire record (header +
@@ -510,12 +555,20 @@ def open_over_ranks(D, res, plaintext_bytes):
     total = D.sum(float(plaintext_bytes))
     if err:
         return err
-    t = max(float(r["ms"]) for r in ranks)
+    # the ranks' calls overlap on a shared GPU: a per-call median then counts the other ranks'
+    # work inside each call, so the job's rate comes from wall-clock-timed runs of successive
+    # calls (open_concurrent_rate) where every rank has one
+    wall = all("concurrent" in r for r in ranks)
+    t = max(float(r["concurrent"]["ms"] if wall else r["ms"]) for r in ranks)
     out = dict(ranks[0])
     out.update({"value": round(total / GIB / (t / 1e3), 2), "ms": round(t, 4),
-                "roundtrip_exact": all(bool(r["roundtrip_exact"]) for r in ranks),
-                "ranks": [{"value": r["value"], "ms": r["ms"], "roundtrip_exact": r["roundtrip_exact"]} for r in ranks],
-                "aggregate": "sum of the ranks' plaintext bytes / the slowest rank's median call time"})
+                "roundtrip_exact": all(bool(r["roundtrip_exact"]) and
+                                       bool(r.get("concurrent", {}).get("roundtrip_exact", True)) for r in ranks),
+                "ranks": [{"value": r["value"], "ms": r["ms"], "roundtrip_exact": r["roundtrip_exact"],
+                           "concurrent_ms": (r.get("concurrent") or {}).get("ms")} for r in ranks],
+                "aggregate": "sum of the ranks' plaintext bytes / the slowest rank's %s" %
+                             ("wall time per call over its successive concurrent calls" if wall
+                              else "median call time")})
     return out
 
 
@@ -893,6 +946,8 @@ def main():
             fr = frame_rate(wl, stream, args.steps)
             if fr is not None:
                 open_res["frame"] = fr
+            if wl.uses_split_pipeline():
+                open_res["concurrent"] = open_concurrent_rate(wl, max(4, min(args.steps, 20)))
         except Exception as e:  # reported, never silently replaced
             open_res = {"error": str(e)}
         if D.world > 1:
