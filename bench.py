@@ -432,49 +432,74 @@ def open_rate(wl, stream, steps):
     return out
 
 
-def open_concurrent_rate(wl, calls, nstreams=2):
+def open_concurrent_rate(wl, calls, nstreams=2, D=None):
     """Successive independent open calls (each against its own copy of the initial read
     states: batches of different connections) issued round-robin on `nstreams` streams of
     different priorities, so one call's MAC pass can run beside the next call's decrypt;
     wall time from the first call to the last stream's synchronize.  Every call's status and
-    each stream's plaintext arena are checked."""
+    each stream's plaintext arena are checked.  With D (N > 1 ranks) every rank must call it:
+    the timed section is bracketed by barriers (each rank's wall time covers the same interval
+    of the job), reached by every rank whatever fails (errors are reported, not raised)."""
     from tlslite_amd import _native as N
     from tlslite_amd.device import DeviceBuffer, Stream, synchronize
     from tlslite_amd.recordlayer import open_dev, open_workspace_bytes
-    calls = max(nstreams, min(int(calls), max(nstreams, int((24 << 30) // max(1, wl.d_states0.nbytes)))))
-    streams = [Stream(high=(i == 0)) for i in range(nstreams)]
-    states = [DeviceBuffer(wl.d_states0.nbytes) for _ in range(calls)]
-    for st in states:
-        N.call("tlsgpu_memcpy_d2d", st.ptr, wl.d_states0.ptr, st.nbytes, None)
-    pts = [wl.d_opt] + [DeviceBuffer(wl.d_opt.nbytes) for _ in range(nstreams - 1)]
-    wss = [[DeviceBuffer(max(open_workspace_bytes(wl.n_records), 16)) for _ in wl.launches] for _ in range(nstreams)]
-    stat = [DeviceBuffer(4 * wl.n_records) for _ in range(calls)]
-    synchronize()
-
-    def one(k, st):
-        i = k % nstreams
-        for j, (var, d_ch, nch) in enumerate(wl.launches):
-            open_dev(d_ch, nch, wl.d_orecs, wl.n_records, wl.d_wire, pts[i], st, stat[k], var, wss[i][j], streams[i])
-    t0 = time.perf_counter()
-    for k in range(calls):
-        one(k, states[k])
-    for s_ in streams:
-        s_.synchronize()
-    t = time.perf_counter() - t0
-    want = wl.pt_len.astype(np.int32)
-    ok = all(bool(np.array_equal(x.download().view(np.int32), want)) for x in stat)
-    saved = wl.d_opt
+    err, bufs = None, []
     try:
-        for p_ in pts:
-            wl.d_opt = p_
-            ok = ok and wl.opened_plaintext_matches()
-    finally:
-        wl.d_opt = saved
-    for b in states + stat + pts[1:] + [w for ws in wss for w in ws]:
+        calls = max(nstreams, min(int(calls), max(nstreams, int((24 << 30) // max(1, wl.d_states0.nbytes)))))
+        streams = [Stream(high=(i == 0)) for i in range(nstreams)]
+        states = [DeviceBuffer(wl.d_states0.nbytes) for _ in range(calls)]
+        for st in states:
+            N.call("tlsgpu_memcpy_d2d", st.ptr, wl.d_states0.ptr, st.nbytes, None)
+        pts = [wl.d_opt] + [DeviceBuffer(wl.d_opt.nbytes) for _ in range(nstreams - 1)]
+        wss = [[DeviceBuffer(max(open_workspace_bytes(wl.n_records), 16)) for _ in wl.launches]
+               for _ in range(nstreams)]
+        stat = [DeviceBuffer(4 * wl.n_records) for _ in range(calls)]
+        bufs = states + stat + pts[1:] + [w for ws in wss for w in ws]
+        synchronize()
+    except Exception as e:  # reported after the collective below
+        err = e
+    ready = (err is None) if D is None else D.sum(0.0 if err is None else 1.0) == 0.0
+    if not ready:
+        for b in bufs:
+            b.free()
+        return {"error": str(err) if err is not None else "another rank could not prepare the concurrent opens"}
+    if D is not None:
+        D.barrier()
+    t0 = time.perf_counter()
+    try:
+        for k in range(calls):
+            i = k % nstreams
+            for j, (var, d_ch, nch) in enumerate(wl.launches):
+                open_dev(d_ch, nch, wl.d_orecs, wl.n_records, wl.d_wire, pts[i], states[k], stat[k], var, wss[i][j],
+                         streams[i])
+        for s_ in streams:
+            s_.synchronize()
+    except Exception as e:
+        err = e
+    if D is not None:
+        D.barrier()
+    t = time.perf_counter() - t0
+    ok = False
+    if err is None:
+        want = wl.pt_len.astype(np.int32)
+        ok = all(bool(np.array_equal(x.download().view(np.int32), want)) for x in stat)
+        saved = wl.d_opt
+        try:
+            for p_ in pts:
+                wl.d_opt = p_
+                ok = ok and wl.opened_plaintext_matches()
+        finally:
+            wl.d_opt = saved
+    for b in bufs:
         b.free()
+    if err is not None:
+        return {"error": str(err)}
     ms = t / calls * 1e3
     return {"value": round(wl.plaintext_total / GIB / (ms / 1e3), 2), "ms": round(ms, 4), "calls": calls,
-            "streams": nstreams, "roundtrip_exact": ok}
+            "streams": nstreams, "roundtrip_exact": ok,
+            "method": "independent opens of the sealed batch (each against its own copy of the read states) issued "
+                      "round-robin on %d streams; wall time / calls%s" %
+                      (nstreams, ", between barriers over all ranks" if D is not None else "")}
 
 
 def frame_rate(wl, stream, steps):
@@ -558,7 +583,7 @@ def open_over_ranks(D, res, plaintext_bytes):
     # the ranks' calls overlap on a shared GPU: a per-call median then counts the other ranks'
     # work inside each call, so the job's rate comes from wall-clock-timed runs of successive
     # calls (open_concurrent_rate) where every rank has one
-    wall = all("concurrent" in r for r in ranks)
+    wall = all("ms" in (r.get("concurrent") or {}) for r in ranks)
     t = max(float(r["concurrent"]["ms"] if wall else r["ms"]) for r in ranks)
     out = dict(ranks[0])
     out.update({"value": round(total / GIB / (t / 1e3), 2), "ms": round(t, 4),
@@ -946,10 +971,12 @@ def main():
             fr = frame_rate(wl, stream, args.steps)
             if fr is not None:
                 open_res["frame"] = fr
-            if wl.uses_split_pipeline():
-                open_res["concurrent"] = open_concurrent_rate(wl, max(4, min(args.steps, 20)))
         except Exception as e:  # reported, never silently replaced
             open_res = {"error": str(e)}
+        if wl.uses_split_pipeline():  # every rank calls it (collectives inside)
+            conc_res = open_concurrent_rate(wl, max(4, min(args.steps, 20)), D=D if D.world > 1 else None)
+            if open_res is not None and "error" not in open_res:
+                open_res["concurrent"] = conc_res
         if D.world > 1:
             open_res = open_over_ranks(D, open_res, wl.plaintext_total)
 
