@@ -4,7 +4,7 @@
 // body, drop the explicit IV, check the padding, compute the MAC with the next
 // seqnum, compare.  Only the seqnum and the CBC residue are serial per
 // connection, and CBC *decryption* is parallel over blocks (P_i = D(C_i) ^ C_{i-1},
-// every C known up front), so the open path is four launches:
+// every C known up front), so the open path is five launches:
 //
 //   open_prefix_kernel  one lane per chain: length checks (:964-977), the
 //                       predecessor ciphertext block of every record's first
