@@ -707,6 +707,41 @@ def probe_device_count():
     return int(r.stdout.strip().splitlines()[-1])
 
 
+def pinned_visibility(env, local_rank, ndev):
+    """The visibility setting that leaves a rank only its own GPU: (variable, value), the
+    local_rank-th entry of the list HIP already applies (HIP_VISIBLE_DEVICES, else
+    CUDA_VISIBLE_DEVICES, which HIP also honours), or HIP_VISIBLE_DEVICES = local_rank when
+    neither is set.  None when the node has fewer GPUs than that rank needs."""
+    if local_rank >= ndev:
+        return None
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None and v.strip():
+            ids = [x.strip() for x in v.split(",") if x.strip()]
+            return (var, ids[local_rank]) if local_rank < len(ids) else None
+    return ("HIP_VISIBLE_DEVICES", str(local_rank))
+
+
+def pin_rank_device(args, D):
+    """One process per GPU, each seeing only its own.  With N > 1 ranks on a node with a GPU
+    for every local rank (no --share-devices), rank i narrows HIP's visible devices to the
+    i-th one before this process makes any GPU call (the count comes from a child process),
+    so every rank drives device 0 of its own view: the library's per-device state (LDS
+    attributes, CU counts, owned workspaces, the split open's second streams) is only used on
+    device 0, the configuration the one-GPU box tests.  TLSGPU_PIN_DEVICE=0 turns it off,
+    =1 forces it at N = 1 too.  Returns "VAR=value" as set, or None."""
+    force = os.environ.get("TLSGPU_PIN_DEVICE")
+    if force == "0" or args.share_devices or os.environ.get("TLSGPU_SHARE_DEVICES") == "1":
+        return None
+    if D.world <= 1 and force != "1":
+        return None
+    pv = pinned_visibility(os.environ, D.local, probe_device_count())
+    if pv is None:
+        return None  # main() refuses the run (too few GPUs), as without pinning
+    os.environ[pv[0]] = pv[1]
+    return "%s=%s" % pv
+
+
 def spawn_ranks(args):
     """--gpus N > 1 without a launcher: one child process per rank (RANK = LOCAL_RANK = i,
     WORLD_SIZE = N, a free rendezvous port on 127.0.0.1), started before this process
@@ -794,18 +829,22 @@ def main():
               file=sys.stderr)
     if args.dry_run:
         return dry_run(args, D)
+    pinned = pin_rank_device(args, D)  # before the first GPU call of this process
     from tlslite_amd import _native as N
     from tlslite_amd.device import Event, Stream, set_device, synchronize, device_count, arch
     ndev = device_count()
     if ndev < 1:
         raise SystemExit("bench.py: no GPU visible to libtlsgpu.so")
-    if D.world > ndev and not args.share_devices and os.environ.get("TLSGPU_SHARE_DEVICES") != "1":
+    shared = pinned is None and D.world > ndev
+    if shared and not args.share_devices and os.environ.get("TLSGPU_SHARE_DEVICES") != "1":
         raise SystemExit("bench.py: %d ranks but only %d GPU(s) visible; pass --share-devices to share them "
                          "round-robin (a rehearsal, not a scaling measurement)" % (D.world, ndev))
-    dev = device_for_rank(D.local, ndev)
+    dev = 0 if pinned else device_for_rank(D.local, ndev)
     set_device(dev)
     dev_arch = arch(dev)
-    progress("rank %d/%d on device %d: building %s" % (D.rank, D.world, dev, args.config))
+    progress("rank %d/%d on device %d%s: building %s" % (D.rank, D.world, dev,
+                                                        " (%s)" % pinned if pinned else "", args.config))
+    pins = D.gather_bytes((pinned or "").encode()) if D.world > 1 else [(pinned or "").encode()]
     wl = build_workload(args.config, D.rank, D.world, args.records, args.pt_align)
     stream = Stream()
     wl.to_device(stream)
@@ -1019,8 +1058,10 @@ def main():
             "config": {"workload": wl.name, "records_per_gpu": wl.n_records,
                        "plaintext_bytes_per_gpu": wl.plaintext_total,
                        "parallelism": "connection-sharded x%d (no collective)" % D.world,
-                       "devices_shared": D.world > ndev,
-                       "device": dev_arch},
+                       "devices_shared": shared,
+                       "device": dev_arch,
+                       # per rank: the visible-device setting it narrowed itself to (pin_rank_device)
+                       "device_pinning": [p.decode() or None for p in pins]},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": wl.dominant_kernel(), "kernel_avg_ms": round(avg_ms, 4),

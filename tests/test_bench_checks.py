@@ -144,3 +144,18 @@ def test_derive_and_host_legs_aggregated_over_ranks():
           "pageable": {"value": 30.0, "ms": 33.0, "bit_exact": False}}
     assert bench.host_inclusive_over_ranks(_FakeRanks([h, hb], [gib, gib]), h, gib)["bit_exact"] is False
     assert "error" in bench.host_inclusive_over_ranks(_FakeRanks([h, None], [gib, gib]), h, gib)
+
+
+def test_pinned_visibility_narrows_to_the_ranks_own_gpu():
+    """pin_rank_device's choice: the local rank's entry of the list HIP already applies, or
+    HIP_VISIBLE_DEVICES = local rank; nothing when the node lacks a GPU for the rank."""
+    import bench
+    pv = bench.pinned_visibility
+    assert pv({}, 0, 8) == ("HIP_VISIBLE_DEVICES", "0")
+    assert pv({}, 7, 8) == ("HIP_VISIBLE_DEVICES", "7")
+    assert pv({}, 1, 1) is None
+    assert pv({"HIP_VISIBLE_DEVICES": "4,5,6,7"}, 2, 4) == ("HIP_VISIBLE_DEVICES", "6")
+    assert pv({"CUDA_VISIBLE_DEVICES": "3, 1"}, 1, 2) == ("CUDA_VISIBLE_DEVICES", "1")
+    assert pv({"HIP_VISIBLE_DEVICES": "2", "CUDA_VISIBLE_DEVICES": "0,1"}, 0, 1) == ("HIP_VISIBLE_DEVICES", "2")
+    assert pv({"HIP_VISIBLE_DEVICES": ""}, 1, 2) == ("HIP_VISIBLE_DEVICES", "1")
+    assert pv({"HIP_VISIBLE_DEVICES": "0"}, 1, 2) is None
