@@ -79,6 +79,10 @@ def parse():
     ap.add_argument("--open-split", default=None, choices=["auto", "chains", "none", "blocks"],
                     help="force the open path's split form (tlsgpu_set_open_parts; default: the library's choice)")
     ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
+    ap.add_argument("--kernel-events-every", type=int, default=None,
+                    help="bracket the dominant kernel with HIP timing events on every M-th timed step (the steps "
+                         "k with k %% M == M // 2); each pair of event records costs ~25 us of the cipher stream's "
+                         "time per step (DESIGN.md section 4).  Default 4 (cfg4, 0.12 s per step: 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="minimum CPU time of the cpu_baseline sample (the full batch, repeated)")
     a = ap.parse_args()
@@ -88,7 +92,17 @@ def parse():
         a.steps = 10 if a.config == "cfg4" else 500
     if a.warmup is None:
         a.warmup = 2 if a.config == "cfg4" else 500
+    if a.kernel_events_every is None:
+        a.kernel_events_every = 1 if a.config == "cfg4" else 4
+    a.kernel_events_every = max(1, a.kernel_events_every)
     return a
+
+
+def event_steps(steps, every):
+    """The timed steps whose dominant kernel is bracketed by HIP events: k % every == every // 2
+    (spread over the run, centred), at least one."""
+    ks = [k for k in range(steps) if k % every == every // 2]
+    return ks or [steps // 2]
 
 
 # The reference's own pure-Python path (BASELINE.md, measured in the survey container through
@@ -893,7 +907,10 @@ def main():
     synchronize()
     D.barrier()
     synchronize()
-    kev = [(Event(), Event()) for _ in range(args.steps)]
+    # HIP events around the dominant kernel on a spread sample of the timed steps (every M-th):
+    # each pair of records adds ~25 us to the cipher stream's step
+    ev_steps = event_steps(args.steps, args.kernel_events_every)
+    kev = {k: (Event(), Event()) for k in ev_steps}
     # RC4 / 3DES-only batches (cfg5) have no phases to overlap: their per-variant seal
     # kernels run concurrently on two streams (disjoint connection states), each step's
     # launch ordered after the previous step's launch of the same variant
@@ -907,11 +924,13 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         if conc:
-            kev[k][0].record(conc[0])
+            if k in kev:
+                kev[k][0].record(conc[0])
             wl.launch(conc)
-            kev[k][1].record(conc[0])
+            if k in kev:
+                kev[k][1].record(conc[0])
         else:
-            wl.launch(pipeline=pipe, cipher_events=kev[k])
+            wl.launch(pipeline=pipe, cipher_events=kev.get(k))
     pipe.synchronize()
     if conc:
         for s_ in conc:
@@ -920,7 +939,7 @@ def main():
     wall = time.perf_counter() - t0
     D.barrier()
     n_state_launches += args.steps
-    per_launch = [a.elapsed_ms(b) for a, b in kev]
+    per_launch = [kev[k][0].elapsed_ms(kev[k][1]) for k in ev_steps]
     pipe.close()
 
     # ---- the timed output itself: replay the same number of seals one call at a time
@@ -1067,6 +1086,9 @@ def main():
                          "kernel": wl.dominant_kernel(), "kernel_avg_ms": round(avg_ms, 4),
                          # the timed steps' kernel times in order: a short run's first steps run
                          # at the clocks of a GPU that has just started working
+                         # the timed steps whose kernel the events bracket: k % every == every // 2
+                         "kernel_events": {"every": args.kernel_events_every, "steps": len(ev_steps),
+                                           "first": ev_steps[0], "last": ev_steps[-1]},
                          "kernel_ms_steps": {"first": round(per_launch[0], 4),
                                              "median": round(float(np.median(per_launch)), 4),
                                              "last": round(per_launch[-1], 4),
