@@ -159,3 +159,13 @@ def test_pinned_visibility_narrows_to_the_ranks_own_gpu():
     assert pv({"HIP_VISIBLE_DEVICES": "2", "CUDA_VISIBLE_DEVICES": "0,1"}, 0, 1) == ("HIP_VISIBLE_DEVICES", "2")
     assert pv({"HIP_VISIBLE_DEVICES": ""}, 1, 2) == ("HIP_VISIBLE_DEVICES", "1")
     assert pv({"HIP_VISIBLE_DEVICES": "0"}, 1, 2) is None
+
+
+def test_event_steps_spread_over_the_timed_region():
+    """The timed steps whose dominant kernel bench.py brackets with HIP events."""
+    import bench
+    assert bench.event_steps(20, 4) == [2, 6, 10, 14, 18]
+    assert bench.event_steps(500, 4)[:3] == [2, 6, 10] and len(bench.event_steps(500, 4)) == 125
+    assert bench.event_steps(10, 1) == list(range(10))
+    assert bench.event_steps(1, 4) == [0]
+    assert bench.event_steps(2, 4) == [1]
