@@ -82,7 +82,7 @@ def parse():
     ap.add_argument("--kernel-events-every", type=int, default=None,
                     help="bracket the dominant kernel with HIP timing events on every M-th timed step (the steps "
                          "k with k %% M == M // 2); each pair of event records costs ~25 us of the cipher stream's "
-                         "time per step (DESIGN.md section 4).  Default 4 (cfg4, 0.12 s per step: 1)")
+                         "time per step (DESIGN.md section 4).  Default 4 (cfg4, cfg5: 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="minimum CPU time of the cpu_baseline sample (the full batch, repeated)")
     a = ap.parse_args()
@@ -93,7 +93,9 @@ def parse():
     if a.warmup is None:
         a.warmup = 2 if a.config == "cfg4" else 500
     if a.kernel_events_every is None:
-        a.kernel_events_every = 1 if a.config == "cfg4" else 4
+        # cfg4 (0.12 s steps) and cfg5 (its events span the whole 4.7-ms 3DES call, so a sampled
+        # step would run longer than the average step): every step
+        a.kernel_events_every = 1 if a.config in ("cfg4", "cfg5") else 4
     a.kernel_events_every = max(1, a.kernel_events_every)
     return a
 
@@ -1088,7 +1090,11 @@ def main():
                          # at the clocks of a GPU that has just started working
                          # the timed steps whose kernel the events bracket: k % every == every // 2
                          "kernel_events": {"every": args.kernel_events_every, "steps": len(ev_steps),
-                                           "first": ev_steps[0], "last": ev_steps[-1]},
+                                           "first": ev_steps[0], "last": ev_steps[-1],
+                                           "span": ("the first variant's whole tlsgpu_seal_dev call on its stream "
+                                                    "(prefix, MAC and cipher kernels: conservative for the "
+                                                    "cipher kernel alone)") if conc else
+                                                   "the cipher kernel alone (tlsgpu_pipeline_seal's cipher events)"},
                          "kernel_ms_steps": {"first": round(per_launch[0], 4),
                                              "median": round(float(np.median(per_launch)), 4),
                                              "last": round(per_launch[-1], 4),
