@@ -478,7 +478,8 @@ def open_concurrent_rate(wl, calls, nstreams=2, D=None):
     if not ready:
         for b in bufs:
             b.free()
-        return {"error": str(err) if err is not None else "another rank could not prepare the concurrent opens"}
+        return (leg_error(err) if err is not None else
+                {"error": "another rank could not prepare the concurrent opens"})
     if D is not None:
         D.barrier()
     t0 = time.perf_counter()
@@ -509,7 +510,7 @@ def open_concurrent_rate(wl, calls, nstreams=2, D=None):
     for b in bufs:
         b.free()
     if err is not None:
-        return {"error": str(err)}
+        return leg_error(err)
     ms = t / calls * 1e3
     return {"value": round(wl.plaintext_total / GIB / (ms / 1e3), 2), "ms": round(ms, 4), "calls": calls,
             "streams": nstreams, "roundtrip_exact": ok,
@@ -579,6 +580,25 @@ def frame_rate(wl, stream, steps):
             "open_from_frames_value": round(wl.plaintext_total / GIB / (tfo / 1e3), 2), "open_from_frames_exact": opened,
             "method": "tlsgpu_frame_dev over each connection's received record in the sealed wire arena, then "
                       "tlsgpu_open_dev on the framed descriptors; medians of HIP-event-timed calls"}
+
+
+def leg_error(e):
+    """A side leg's failure as its JSON field.  hip_error marks a failed HIP call (TLSGPU_EHIP:
+    a fault such as an illegal memory access leaves the device context dead): the run then
+    ends with a non-zero exit status after its line is printed (hip_failures)."""
+    from tlslite_amd import _native as N
+    return {"error": str(e), "hip_error": getattr(e, "code", None) == N.EHIP}
+
+
+def hip_failures(legs):
+    """Names of the legs (dict name -> result) that hit a HIP error on any rank."""
+    def bad(r):
+        if isinstance(r, dict):
+            return bool(r.get("hip_error")) or any(bad(v) for v in r.values())
+        if isinstance(r, list):
+            return any(bad(v) for v in r)
+        return False
+    return [k for k, r in legs.items() if bad(r)]
 
 
 def _leg_ranks(D, res, leg):
@@ -1032,7 +1052,7 @@ def main():
             if fr is not None:
                 open_res["frame"] = fr
         except Exception as e:  # reported, never silently replaced
-            open_res = {"error": str(e)}
+            open_res = leg_error(e)
         if wl.uses_split_pipeline():  # every rank calls it (collectives inside)
             conc_res = open_concurrent_rate(wl, max(4, min(args.steps, 20)), D=D if D.world > 1 else None)
             if open_res is not None and "error" not in open_res:
@@ -1047,7 +1067,7 @@ def main():
             progress("derive leg")
             derive_res = derive_rate(stream)
         except Exception as e:  # reported, never silently replaced
-            derive_res = {"error": str(e)}
+            derive_res = leg_error(e)
         if D.world > 1:
             derive_res = derive_over_ranks(D, derive_res)
 
@@ -1057,7 +1077,7 @@ def main():
         try:
             host_inc = host_inclusive_rate(wl)
         except Exception as e:  # reported, never silently replaced
-            host_inc = {"error": str(e)}
+            host_inc = leg_error(e)
         if D.world > 1 and D.sum(0.0 if host_inc is None else 1.0) > 0:  # None: a multi-variant batch
             host_inc = host_inclusive_over_ranks(D, host_inc, wl.plaintext_total)
 
@@ -1135,8 +1155,17 @@ def main():
             "open": open_res,
             "derive": derive_res,
         }
+    # a HIP error in any leg (on any rank) fails the run: the device context is dead, and the
+    # line must not read as a successful one
+    failed = hip_failures({"open": open_res, "derive": derive_res, "host_inclusive": host_inc})
+    if D.rank == 0:
+        if failed:
+            out["error"] = "HIP error in the %s leg(s); the run failed" % ", ".join(failed)
         print(json.dumps(out))
     D.close()
+    if failed:
+        progress("HIP error in the %s leg(s): exiting with status 1" % ", ".join(failed))
+        sys.exit(1)
 
 
 if __name__ == "__main__":

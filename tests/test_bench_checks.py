@@ -169,3 +169,19 @@ def test_event_steps_spread_over_the_timed_region():
     assert bench.event_steps(10, 1) == list(range(10))
     assert bench.event_steps(1, 4) == [0]
     assert bench.event_steps(2, 4) == [1]
+
+
+def test_hip_error_in_a_leg_fails_the_run():
+    """A failed HIP call in a side leg (TLSGPU_EHIP: the context is dead after a fault) is
+    marked in the leg's field and named by hip_failures, which makes bench.py exit non-zero;
+    other leg errors (an unsupported shape, a refused argument) are reported, not fatal."""
+    import bench
+    from tlslite_amd import _native as N
+    hip = bench.leg_error(N.TLSGPUError(N.EHIP, "tlsgpu_stream_synchronize"))
+    inval = bench.leg_error(N.TLSGPUError(N.EINVAL, "tlsgpu_open_dev"))
+    assert hip["hip_error"] and not inval["hip_error"]
+    assert bench.hip_failures({"open": hip, "derive": None}) == ["open"]
+    assert bench.hip_failures({"open": inval, "derive": {"ms": 1.0}}) == []
+    # N > 1: a rank's failure nested in the aggregated leg
+    agg = {"error": "open leg failed on rank(s) [1]", "ranks": [{"value": 1.0}, hip]}
+    assert bench.hip_failures({"open": agg, "host_inclusive": None}) == ["open"]

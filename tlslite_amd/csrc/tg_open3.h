@@ -229,6 +229,14 @@ __device__ __forceinline__ uint64_t open_dec_batch(const OpenMeta* meta, uint32_
     return __ballot(mine);
 }
 
+// Word v of lane l as an unsigned value: __builtin_amdgcn_readlane returns int, and a plain
+// (uint64_t) cast of it sign-extends -- round 5's 64-bit offsets rebuilt that way turned every
+// low word >= 2^31 into 0xffffffff'xxxxxxxx, the illegal address of cfg4's open (arenas > 2 GiB)
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint64_t lane_u64(uint32_t v, int lo) {
+    return (uint64_t)lane_u32(v, lo) | ((uint64_t)lane_u32(v, lo + 1) << 32);
+}
+
 // Lane l of wave-wide value v from lane l - 1 (DPP wave_shr:1, one VALU); lane 0 gets `first`
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t first) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xf, 0xf, false);
@@ -287,7 +295,7 @@ template <int NR>
 __device__ __forceinline__ uint32_t open_fetch_keys(const ConnState* states, uint32_t vm, uint32_t r) {
     const uint32_t lane = __lane_id();
     if (r == ~0u) return 0u;
-    const ConnState* st = states + __builtin_amdgcn_readlane(vm, 6);  // OpenMeta.state
+    const ConnState* st = states + lane_u32(vm, 6);  // OpenMeta.state
     if (lane < 4 * (NR + 1)) return st->dk[lane];
     if (lane == 63) return st->explicit_iv;
     return 0u;
@@ -328,16 +336,14 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
         // this record's descriptor and keys, wave-uniform
         uint32_t dk[4 * (NR + 1)];
 #pragma unroll
-        for (int i = 0; i < 4 * (NR + 1); i++) dk[i] = __builtin_amdgcn_readlane(vk, i);
-        const uint32_t E = __builtin_amdgcn_readlane(vk, 63) ? 16u : 0u;
+        for (int i = 0; i < 4 * (NR + 1); i++) dk[i] = lane_u32(vk, i);
+        const uint32_t E = lane_u32(vk, 63) ? 16u : 0u;
         uint32_t carry[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) carry[i] = __builtin_amdgcn_readlane(vm, i);  // OpenMeta.pred
-        const uint64_t ct_off = (uint64_t)__builtin_amdgcn_readlane(vm, 12) |
-                                ((uint64_t)__builtin_amdgcn_readlane(vm, 13) << 32);
-        const uint64_t pt_off = (uint64_t)__builtin_amdgcn_readlane(vm, 14) |
-                                ((uint64_t)__builtin_amdgcn_readlane(vm, 15) << 32);
-        const uint32_t ct_len = __builtin_amdgcn_readlane(vm, 16);
+        for (int i = 0; i < 4; i++) carry[i] = lane_u32(vm, i);  // OpenMeta.pred
+        const uint64_t ct_off = lane_u64(vm, 12);  // tlsgpu_open_record.ct_off
+        const uint64_t pt_off = lane_u64(vm, 14);  // tlsgpu_open_record.pt_off
+        const uint32_t ct_len = lane_u32(vm, 16);
         // the next record's descriptor now; its keys after this record's first chunk
         const uint32_t rn = rs.next();
         vm = open_fetch_desc(meta, recs, rn);
@@ -358,7 +364,7 @@ open_aes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords, 
 #pragma unroll
                 for (int i = 0; i < 4; i++) {
                     p[i] = wave_shr1(c[i], carry[i]);
-                    carry[i] = __builtin_amdgcn_readlane(c[i], 63);  // the next chunk's lane-0 predecessor
+                    carry[i] = lane_u32(c[i], 63);  // the next chunk's lane-0 predecessor
                 }
                 if (b < hi) {
                     uint32_t d[4] = {c[0], c[1], c[2], c[3]};
@@ -479,7 +485,7 @@ open_tdes_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
 #pragma unroll
             for (int i = 0; i < 2; i++) {
                 p[i] = wave_shr1(c[i], carry[i]);
-                carry[i] = __builtin_amdgcn_readlane(c[i], 63);
+                carry[i] = lane_u32(c[i], 63);
             }
             if (b < hi) {
                 uint32_t whi = bswap32(c[0]), wlo = bswap32(c[1]);
