@@ -402,6 +402,102 @@ def host_inclusive_rate(wl, chunk=64 << 20, depth=3):
     return out
 
 
+def compact_rx(wl):
+    """The sealed batch as connections' received bytes: each connection's wire records back to
+    back (what its socket delivers) in one host arena, connections one after another.  ->
+    (arena, per-connection offsets and lengths, per-record body offsets in the arena)."""
+    lens = wl.wire_len.astype(np.int64)
+    n_conn = wl.n_chains
+    conn_bytes = np.array([int(lens[int(f):int(f) + int(c)].sum()) for f, c in zip(wl.chain_first, wl.chain_count)],
+                          dtype=np.int64)
+    conn_off = np.concatenate([[0], np.cumsum(conn_bytes)[:-1]]).astype(np.int64)
+    rec_pos = np.empty(wl.n_records, dtype=np.int64)  # record r's header in the compact arena
+    for c in range(n_conn):
+        f, k = int(wl.chain_first[c]), int(wl.chain_count[c])
+        rec_pos[f:f + k] = conn_off[c] + np.concatenate([[0], np.cumsum(lens[f:f + k])[:-1]])
+    return conn_off, conn_bytes, rec_pos
+
+
+def host_open_rate(wl, link=None, chunk=64 << 20, depth=3):
+    """Open with the records starting in HOST socket buffers and the plaintext ending there
+    (tlsgpu_host_pipeline_open: H2D of the received bytes, framing and open on the device, D2H
+    of the plaintext, sub-batches of ~chunk bytes overlapped), pinned and pageable host arenas;
+    every status and every record's plaintext checked.  Wall time of the synchronous call, best
+    of 3.  One-variant batches only.  Never `value`."""
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import PinnedBuffer, synchronize
+    from tlslite_amd.recordlayer import HostSealPipeline
+    if len(wl.launches) != 1:
+        return None
+    var = wl.launches[0][0]
+    wl.reset_states()
+    wl.launch()
+    synchronize()
+    wire = wl.d_wire.download()
+    ref_pt = wl.d_pt.download()
+    conn_off, conn_bytes, rec_pos = compact_rx(wl)
+    nbytes = int(conn_bytes.sum())
+    pin_rx, pin_pt = PinnedBuffer(nbytes), PinnedBuffer(nbytes)
+    rx = pin_rx.array[:nbytes]
+    lens = wl.wire_len.astype(np.int64)
+    for r in range(wl.n_records):  # the received bytes: each record where its connection's stream has it
+        a, w = int(rec_pos[r]), int(wl.wire_off[r])
+        rx[a:a + lens[r]] = wire[w:w + lens[r]]
+    del wire
+    spans = (N.Span * wl.n_chains)()
+    sp = np.frombuffer(spans, dtype=np.uint8).reshape(wl.n_chains, 16)
+    sp[:, 0:8] = conn_off.astype(np.uint64).reshape(-1, 1).view(np.uint8)
+    sp[:, 8:12] = conn_bytes.astype(np.uint32).reshape(-1, 1).view(np.uint8)
+    sp[:, 12:16] = np.arange(wl.n_chains, dtype=np.uint32).reshape(-1, 1).view(np.uint8)
+    link = link or pcie_rates()
+    if link:
+        t_min = max(nbytes / (link["h2d"] * 1e9), nbytes / (link["d2h"] * 1e9), 2 * nbytes / (link["both"] * 1e9))
+        how = "measured pinned hipMemcpyAsync rates on this box (pcie_measured_gbs)"
+    else:
+        t_min = nbytes / (PCIE_GBS * 1e9)
+        how = "63 GB/s per direction, full duplex (spec)"
+    out = {"unit": "GiB/s", "chunk_bytes": chunk, "depth": depth, "bytes_h2d": nbytes, "bytes_d2h": nbytes,
+           "pcie_measured_gbs": link, "pcie_ceiling": round(wl.plaintext_total / GIB / t_min, 2),
+           "method": "tlsgpu_host_pipeline_open: each connection's received records back to back in a host "
+                     "arena; per sub-batch of ~chunk_bytes an H2D copy, framing (as tlsgpu_frame_dev) and open "
+                     "(as tlsgpu_open_dev) on the device, a D2H copy of the plaintext range, descriptors and "
+                     "statuses, `depth` sub-batches in flight; wall time of the synchronous call, best of 3; "
+                     "pcie_ceiling = plaintext / the copies' minimum time at " + how}
+    body = rec_pos + 5
+    want_st = wl.pt_len.astype(np.int32)
+    recs_out = {"records": (N.OpenRecord * (wl.n_records + 1))(), "status": np.zeros(wl.n_records + 1, np.int32)}
+    with HostSealPipeline(chunk, depth) as hp:
+        for name, rx_h, pt_h in (("pinned", rx, pin_pt.array[:nbytes]), ("pageable", rx.copy(), None)):
+            if pt_h is None:
+                pt_h = np.zeros(nbytes, dtype=np.uint8)
+            progress("host-inclusive open, %s arenas" % name)
+            best = None
+            for _rep in range(3):
+                N.call("tlsgpu_memcpy_d2d", wl.d_ostates.ptr, wl.d_states0.ptr, wl.d_ostates.nbytes, None)
+                synchronize()
+                t0 = time.perf_counter()
+                res = hp.open(rx_h, spans, pt_h, wl.d_ostates, var, max_records=wl.n_records + 1, out=recs_out)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            exact = res["total"] == wl.n_records and bool(np.array_equal(res["status"], want_st))
+            if exact:
+                got = np.frombuffer(res["records"], dtype=np.uint8).reshape(-1, 24)[: wl.n_records]
+                exact = bool(np.array_equal(got[:, 0:8].copy().view(np.uint64).ravel(), body.astype(np.uint64)))
+            if exact:
+                for r in range(wl.n_records):
+                    a, b, k = int(body[r]), int(wl.pt_off[r]), int(wl.pt_len[r])
+                    if not np.array_equal(pt_h[a:a + k], ref_pt[b:b + k]):
+                        exact = False
+                        break
+            out[name] = {"value": round(wl.plaintext_total / GIB / best, 2), "ms": round(best * 1e3, 3),
+                         "roundtrip_exact": exact}
+    out["value"] = out["pinned"]["value"]
+    out["pcie_frac"] = round(out["value"] / out["pcie_ceiling"], 3)
+    pin_rx.free()
+    pin_pt.free()
+    return out
+
+
 def open_rate(wl, stream, steps):
     """Open path on the batch: seal once from the initial states, then open it
     with read states reset to the initial ones before every (timed) call."""
@@ -1051,6 +1147,10 @@ def main():
             fr = frame_rate(wl, stream, args.steps)
             if fr is not None:
                 open_res["frame"] = fr
+            if args.host_inclusive:
+                hio = host_open_rate(wl)
+                if hio is not None:
+                    open_res["host_inclusive"] = hio
         except Exception as e:  # reported, never silently replaced
             open_res = leg_error(e)
         if wl.uses_split_pipeline():  # every rank calls it (collectives inside)

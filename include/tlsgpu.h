@@ -21,6 +21,9 @@
  *   tlsgpu_frame_dev ......... tlsrecordlayer.py:832-876 (_getNextRecord's header
  *                              parse; RecordHeader3.parse, messages.py:44-49),
  *                              batched over connections' received bytes
+ *   tlsgpu_host_pipeline_open  the receive path from host socket buffers: the
+ *                              recv loops :832-893, framing and _decryptRecord
+ *                              :958-1044, with the PCIe copies overlapped
  *   tlsgpu_cipher_dev ........ utils/python_aes.py:20-69, utils/python_rc4.py:25-41,
  *                              utils/openssl_tripledes.py:29-47 (the stateful
  *                              cipher-object encrypt/decrypt behind
@@ -59,7 +62,7 @@
 extern "C" {
 #endif
 
-#define TLSGPU_ABI_VERSION 6
+#define TLSGPU_ABI_VERSION 7
 
 /* ---- suite components (tlsrecordlayer.py:1063-1095, constants.py:159-201) */
 enum {
@@ -87,6 +90,10 @@ enum {
     TLSGPU_EMISMATCH = -5,  /* connection state does not match the launch variant */
     TLSGPU_EFRAME = -6,     /* received bytes are not a TLS record header: the first byte is no
                              * content type (tlsrecordlayer.py:850-857 raises SyntaxError) */
+    TLSGPU_EABRUPT = -7,    /* receive framing (ABI 7): a record header announcing an empty body --
+                             * the reference's body loop calls sock.recv(0), gets b"" and raises
+                             * TLSAbruptCloseError (tlsrecordlayer.py:877-889): the connection ends
+                             * there, the empty record is not framed */
     /* open-path per-record status (alerts, tlsrecordlayer.py:964-1042) */
     TLSGPU_ALERT_BAD_RECORD_MAC = -20,
     TLSGPU_ALERT_DECRYPTION_FAILED = -21,
@@ -355,7 +362,34 @@ int tlsgpu_open_dev(const tlsgpu_chain *chains, uint32_t nchains, const tlsgpu_o
 enum { TLSGPU_OPEN_SPLIT_AUTO = 0, TLSGPU_OPEN_SPLIT_CHAINS = 1, TLSGPU_OPEN_SPLIT_NONE = 2,
        TLSGPU_OPEN_SPLIT_BLOCKS = 3 };
 int tlsgpu_set_open_parts(int mode, int64_t min_records);
-/* ---- receive framing on the device (ABI 6, round 5): _getNextRecord's header parse
+/* Receive path from HOST socket buffers (ABI 7): connection i's received bytes are
+ * rx_host[conns[i].off, + conns[i].len) -- what the reference's sock.recv loops gather
+ * (tlsrecordlayer.py:832-893) -- and they are framed (as tlsgpu_frame_dev) and opened (as
+ * tlsgpu_open_dev, :958-1044) on the device, in sub-batches of consecutive connections of
+ * about chunk_bytes received bytes: H2D copy, framing, open and D2H copy of `depth`
+ * sub-batches overlap on the pipeline's streams.  Results, as one tlsgpu_frame_dev +
+ * tlsgpu_open_dev over every connection would give them:
+ *   records_host[0 .. *total_host)  the framed records in connection order (ct_off = pt_off =
+ *                                   the body's offset in rx_host), at most max_records;
+ *   status_host[r]                  record r's open status (plaintext length or TLSGPU_ALERT_*);
+ *   pt_host + pt_off                record r's decrypted body after the explicit IV (payload |
+ *                                   MAC | padding, as tlsgpu_open_dev writes it); pt_bytes >=
+ *                                   rx_bytes.  pt_host bytes of each sub-batch's received range
+ *                                   [first span, last span end) that hold no opened body come
+ *                                   back zero;
+ *   chains_host[i], consumed_host[i], frame_status_host[i]  as tlsgpu_frame_dev's chains /
+ *                                   consumed / status (chains_host[i].first indexes records_host).
+ * states: DEVICE array of nstates read states (updated in place); every connection of the call
+ * must use its own state, of `variant`.  Host arrays may be pinned (copied directly) or
+ * pageable (staged through the pipeline's pinned buffers).  Synchronous. */
+int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t *rx_host, size_t rx_bytes,
+                              const tlsgpu_span *conns, uint32_t n, uint32_t chain_flags, uint8_t *pt_host,
+                              size_t pt_bytes, tlsgpu_conn_state *states, uint32_t nstates, uint32_t variant,
+                              tlsgpu_open_record *records_host, uint32_t max_records, tlsgpu_chain *chains_host,
+                              uint32_t *consumed_host, int32_t *frame_status_host, int32_t *status_host,
+                              uint32_t *total_host);
+/* ---- receive framing on the device (ABI 6, round 5; ABI 7: TLSGPU_EABRUPT, 64-bit
+ * workspace sums): _getNextRecord's header parse
  * (tlsrecordlayer.py:832-876; RecordHeader3.parse, messages.py:44-49) for n connections'
  * received bytes in one arena of stream_bytes, connection i's at [conns[i].off, conns[i].off +
  * conns[i].len).  Each complete record becomes one tlsgpu_open_record {ct_off = pt_off = its
@@ -365,11 +399,14 @@ int tlsgpu_set_open_parts(int mode, int64_t min_records);
  * status[i] = the number of records framed, or TLSGPU_ALERT_RECORD_OVERFLOW (a header
  * announcing more than 18432 body bytes: the records before it are framed, the connection
  * stops there), TLSGPU_EFRAME (a record starting with a byte that is no content type 20-23;
- * SSLv2 headers belong to the handshake, which is out of scope), TLSGPU_EINVAL (the span
+ * SSLv2 headers belong to the handshake, which is out of scope), TLSGPU_EABRUPT (a header
+ * announcing an empty body: the reference raises TLSAbruptCloseError there, so the records
+ * before it are framed and the connection stops), TLSGPU_EINVAL (the span
  * leaves the arena).  Records past max_records are not framed (consumed[] stops before
  * them).  total (device, one uint32) = records framed.  The result feeds tlsgpu_open_dev
  * directly (nrecords = max_records, or *total read back), with a plaintext arena of
- * stream_bytes.  Everything is device memory; workspace: tlsgpu_frame_workspace_bytes(n). */
+ * stream_bytes.  Everything is device memory; workspace: tlsgpu_frame_workspace_bytes(n),
+ * 8-byte aligned. */
 size_t tlsgpu_frame_workspace_bytes(uint32_t n);
 int tlsgpu_frame_dev(const uint8_t *stream, size_t stream_bytes, const tlsgpu_span *conns, uint32_t n,
                      tlsgpu_open_record *records, uint32_t max_records, tlsgpu_chain *chains,

@@ -21,6 +21,7 @@ ALERT_BAD_RECORD_MAC = -20
 ALERT_DECRYPTION_FAILED = -21
 ALERT_RECORD_OVERFLOW = -23
 EFRAME = -6
+EABRUPT = -7
 
 # suite name -> (cipher, key len, iv len, mac, mac len); tlsrecordlayer.py:1063-1095
 SUITES = {
@@ -236,9 +237,10 @@ def frame(data):
     complete record as (content_type, (major, minor), body), stopping at an incomplete record
     (left for the next read), at a first header byte that is no content type (:850-857 --
     SyntaxError as soon as that byte arrives; SSLv2 headers are handshake-only and not
-    framed here), or at a header announcing more than 18432 body bytes (:871-873,
-    record_overflow).  Returns (records, consumed, code): code 0, EFRAME or
-    ALERT_RECORD_OVERFLOW."""
+    framed here), at a header announcing more than 18432 body bytes (:871-873,
+    record_overflow), or at a header announcing an empty body (the body loop's sock.recv(0)
+    returns b"" and raises TLSAbruptCloseError, :877-889).  Returns (records, consumed,
+    code): code 0, EFRAME, ALERT_RECORD_OVERFLOW or EABRUPT."""
     data = bytes(data)
     out, pos = [], 0
     while pos < len(data):
@@ -249,6 +251,8 @@ def frame(data):
         length = (data[pos + 3] << 8) | data[pos + 4]
         if length > 18432:
             return out, pos, ALERT_RECORD_OVERFLOW
+        if length == 0:
+            return out, pos, EABRUPT
         if len(data) - pos - 5 < length:
             break
         out.append((data[pos], (data[pos + 1], data[pos + 2]), data[pos + 5:pos + 5 + length]))

@@ -12,9 +12,9 @@ header or body), "syntax" (SyntaxError: a first header byte that is no content t
 :850-857) or "overflow" (TLSLocalAlert record_overflow, :871-873).  Content types 20, 21
 and 23 only (22 would go on into handshake-message parsing, beyond the record layer's
 framing), no SSLv2 headers (first byte 128, handshake-only: the device framing refuses them
-as a syntax error), and no empty records: the reference cannot receive one -- its body loop
-calls sock.recv(0), gets b"" and raises TLSAbruptCloseError (:880-889) -- while the device
-framing passes a zero-length record on like any other (tests/test_frame.py covers it).
+as a syntax error).  Empty records are in (round 6): the reference's body loop calls
+sock.recv(0), which a socket answers with b"" (the fake socket too), and raises
+TLSAbruptCloseError (:877-889) -- recorded as stop "abrupt" at the empty record's header.
 
 Output: tests/golden/frames.json (inputs as hex).
 Usage:  PYTHONDONTWRITEBYTECODE=1 python3 -B tests/golden/make_frame_golden.py
@@ -37,7 +37,7 @@ pkg.__path__ = [REF]
 sys.modules["tlslite"] = pkg
 
 from tlslite.tlsrecordlayer import TLSRecordLayer  # noqa: E402
-from tlslite.errors import TLSLocalAlert  # noqa: E402
+from tlslite.errors import TLSAbruptCloseError, TLSLocalAlert  # noqa: E402
 
 
 class FakeSock:
@@ -47,6 +47,8 @@ class FakeSock:
         self.data, self.pos, self.sent = bytes(data), 0, bytearray()
 
     def recv(self, n):
+        if n == 0:  # a socket's recv(0) returns b"" at once
+            return b""
         if self.pos >= len(self.data):
             raise socket.error(errno.EWOULDBLOCK, "would block")
         s = self.data[self.pos:self.pos + n]
@@ -89,6 +91,8 @@ def ref_frame(data):
         except TLSLocalAlert as e:
             assert e.description == 22, e  # record_overflow
             return recs, start, "overflow"
+        except TLSAbruptCloseError:
+            return recs, start, "abrupt"
     return recs, sock.pos, stop
 
 
@@ -129,6 +133,11 @@ def cases():
     out.append(("bad_lone_byte", bytes([7])))
     out.append(("overflow_first", header(23, 18433)))
     out.append(("max_body_then_more", rec(rng, 23, 18432) + header(20, 1) ))
+    # empty records (round 6): the connection ends at the first one
+    out.append(("empty_record_first", header(23, 0) + rec(rng, 23, 10)))
+    out.append(("records_then_empty", rec(rng, 23, 300) + rec(rng, 21, 2) + header(23, 0) + rec(rng, 23, 7)))
+    out.append(("empty_record_last", rec(rng, 20, 1) + header(21, 0)))
+    out.append(("empty_handshake_type", rec(rng, 23, 40) + header(20, 0, (3, 1))))
     return out
 
 

@@ -52,13 +52,14 @@ def test_abi_structs_and_constants():
                       ("TLSGPU_MAC_MD5", 3), ("TLSGPU_ALERT_BAD_RECORD_MAC", -20),
                       ("TLSGPU_ALERT_DECRYPTION_FAILED", -21), ("TLSGPU_ALERT_SKIPPED", -22),
                       ("TLSGPU_ALERT_RECORD_OVERFLOW", -23), ("TLSGPU_EFRAME", -6),
-                      ("TLSGPU_CONN_STATE_BYTES", 2048), ("TLSGPU_ABI_VERSION", 6)]:
+                      ("TLSGPU_EABRUPT", -7), ("TLSGPU_CONN_STATE_BYTES", 2048), ("TLSGPU_ABI_VERSION", 7)]:
         assert re.search(r"\b%s\s*=?\s*%d\b" % (name, val), src), name
     assert re.search(r"#define TLSGPU_CHAIN_STOP_ON_ALERT 1u", src)
-    assert N.lib.tlsgpu_abi_version() == N.ABI_VERSION == 6
+    assert N.lib.tlsgpu_abi_version() == N.ABI_VERSION == 7
     assert (N.ALERT_SKIPPED, N.CHAIN_STOP_ON_ALERT) == (-22, 1)
-    assert (N.ALERT_RECORD_OVERFLOW, N.EFRAME) == (-23, -6)
-    assert N.lib.tlsgpu_frame_workspace_bytes(1000) >= 4 * 1000
+    assert (N.ALERT_RECORD_OVERFLOW, N.EFRAME, N.EABRUPT) == (-23, -6, -7)
+    # per connection a 32-bit count, per 256 connections a 64-bit sum (ABI 7)
+    assert N.lib.tlsgpu_frame_workspace_bytes(1000) >= 4 * 1000 + 8 * 4
     assert ctypes.sizeof(N.Record) == 24 and ctypes.sizeof(N.Chain) == 16
     assert [f[0] for f in N.Chain._fields_] == ["state", "first", "count", "flags"]
 

@@ -17,7 +17,7 @@ GOLD = json.load(open(os.path.join(HERE, "golden", "frames.json")))["cases"]
 
 
 def _code(O, stop):
-    return {"more": 0, "syntax": O.EFRAME, "overflow": O.ALERT_RECORD_OVERFLOW}[stop]
+    return {"more": 0, "syntax": O.EFRAME, "overflow": O.ALERT_RECORD_OVERFLOW, "abrupt": O.EABRUPT}[stop]
 
 
 def _random_stream(rng, nrec, tail):
@@ -55,7 +55,8 @@ def test_oracle_frame_matches_reference_goldens():
 
 def test_parse_records_matches_reference_goldens():
     from oracle import oracle as O
-    from tlslite_amd.recordlayer import RecordOverflow, RecordSyntaxError, parse_records
+    from tlslite_amd.recordlayer import RecordAbruptClose, RecordOverflow, RecordSyntaxError, parse_records
+    exc = {"syntax": RecordSyntaxError, "overflow": RecordOverflow, "abrupt": RecordAbruptClose}
     for c in GOLD:
         data = bytes.fromhex(c["hex"])
         if c["stop"] == "more":
@@ -63,30 +64,45 @@ def test_parse_records_matches_reference_goldens():
             assert len(recs) == len(c["records"]) and rest == data[c["consumed"]:], c["name"]
             assert [hashlib.sha256(b).hexdigest() for _, _, b in recs] == [r["sha256"] for r in c["records"]]
         else:
-            with pytest.raises(RecordSyntaxError if c["stop"] == "syntax" else RecordOverflow):
+            with pytest.raises(exc[c["stop"]]):
                 parse_records(data)
         assert O.frame(data)[2] == _code(O, c["stop"])
 
 
+def _expected(O, recs, tail):
+    """(records, consumed, code) the framing must give for a _random_stream: every record up
+    to the first empty one, where the connection ends (TLSAbruptCloseError in the reference),
+    else every record and the tail's code."""
+    for i, (_, b) in enumerate(recs):
+        if not b:
+            return recs[:i], sum(5 + len(x) for _, x in recs[:i]), O.EABRUPT
+    code = {"": 0, "hdr": 0, "body": 0, "bad": O.EFRAME, "over": O.ALERT_RECORD_OVERFLOW}[tail]
+    return recs, sum(5 + len(x) for _, x in recs), code
+
+
 def test_oracle_frame_random_streams_and_empty_records():
-    """The oracle on streams the goldens cannot hold (empty records) agrees with the
-    host parse_records record for record."""
+    """The oracle on streams with empty records and every kind of tail agrees with the host
+    parse_records record for record; an empty record ends the connection."""
     from oracle import oracle as O
-    from tlslite_amd.recordlayer import RecordOverflow, RecordSyntaxError, parse_records
+    from tlslite_amd.recordlayer import RecordAbruptClose, RecordOverflow, RecordSyntaxError, parse_records
     rng = np.random.default_rng(7)
+    nabrupt = 0
     for k in range(200):
         tail = ["", "hdr", "body", "bad", "over"][k % 5]
         data, recs = _random_stream(rng, int(rng.integers(0, 6)), tail)
         got, consumed, code = O.frame(data)
-        assert [(t, b) for t, _, b in got] == recs
-        want = {"": 0, "hdr": 0, "body": 0, "bad": O.EFRAME, "over": O.ALERT_RECORD_OVERFLOW}[tail]
-        assert code == want
+        want, wcons, wcode = _expected(O, recs, tail)
+        assert [(t, b) for t, _, b in got] == want and code == wcode
+        assert consumed == wcons
+        nabrupt += code == O.EABRUPT
         if code == 0:
             r2, rest = parse_records(data)
             assert [(t, b) for t, _, b in r2] == recs and rest == data[consumed:]
         else:
-            with pytest.raises(RecordSyntaxError if code == O.EFRAME else RecordOverflow):
+            exc = {O.EFRAME: RecordSyntaxError, O.ALERT_RECORD_OVERFLOW: RecordOverflow, O.EABRUPT: RecordAbruptClose}
+            with pytest.raises(exc[code]):
                 parse_records(data)
+    assert nabrupt >= 10
 
 
 def _check_device(O, streams, res, total, max_records=None):

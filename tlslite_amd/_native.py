@@ -14,11 +14,11 @@ LIB_PATH = os.environ.get("TLSGPU_LIB") or os.path.join(HERE, "lib", "libtlsgpu.
 CIPHER_AES128, CIPHER_AES256, CIPHER_RC4, CIPHER_3DES, CIPHER_AES192 = 1, 2, 3, 4, 5
 MAC_SHA1, MAC_SHA256, MAC_MD5 = 1, 2, 3
 FAULT_BAD_MAC, FAULT_BAD_PADDING = 1, 2
-OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH, EFRAME = 0, -1, -2, -3, -4, -5, -6
+OK, EINVAL, EHIP, ENODEV, ETOOBIG, EMISMATCH, EFRAME, EABRUPT = 0, -1, -2, -3, -4, -5, -6, -7
 ALERT_BAD_RECORD_MAC, ALERT_DECRYPTION_FAILED, ALERT_SKIPPED, ALERT_RECORD_OVERFLOW = -20, -21, -22, -23
 CHAIN_STOP_ON_ALERT = 1
 OPEN_SPLIT_AUTO, OPEN_SPLIT_CHAINS, OPEN_SPLIT_NONE, OPEN_SPLIT_BLOCKS = 0, 1, 2, 3
-ABI_VERSION = 6
+ABI_VERSION = 7
 CONN_STATE_BYTES = 2048
 
 
@@ -108,6 +108,8 @@ SIGNATURES = [
     ("tlsgpu_host_pipeline_create", _i, [ctypes.POINTER(_vp), _sz, _i]),
     ("tlsgpu_host_pipeline_destroy", _i, [_vp]),
     ("tlsgpu_host_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32]),
+    ("tlsgpu_host_pipeline_open", _i, [_vp, _vp, _sz, _vp, _u32, _u32, _vp, _sz, _vp, _u32, _u32, _vp, _u32, _vp, _vp,
+                                       _vp, _vp, _vp]),
     ("tlsgpu_open_workspace_bytes", _sz, [_u32]),
     ("tlsgpu_open_dev", _i, [_vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32, _vp, _sz, _vp]),
     ("tlsgpu_set_open_parts", _i, [_i, ctypes.c_int64]),

@@ -613,6 +613,14 @@ struct tlsgpu_host_pipeline_s {
     DevBuf pt, wire, recs, chains, len;
     std::vector<DevBuf> ws;
     std::vector<PinBuf> pt_stage, wire_stage;
+    // receive direction (tlsgpu_host_pipeline_open): the received bytes and the opened
+    // plaintext (device arenas mirroring the host ones), the connections' spans and framing
+    // results, and per slot the framed descriptors, statuses and workspaces of one sub-batch
+    DevBuf rx, opt, conns, rchains, consumed, fstatus, totals;
+    std::vector<DevBuf> rrecs, rstat, rws, fws;
+    std::vector<PinBuf> rx_stage, opt_stage, recs_stage, stat_stage;
+    PinBuf h_totals;
+    std::vector<hipEvent_t> framed, opened;
 };
 
 int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, int depth) {
@@ -629,6 +637,16 @@ int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, i
     p->pt_stage.resize(depth);
     p->wire_stage.resize(depth);
     p->mac_done.resize(depth);
+    p->rrecs.resize(depth);
+    p->rstat.resize(depth);
+    p->rws.resize(depth);
+    p->fws.resize(depth);
+    p->rx_stage.resize(depth);
+    p->opt_stage.resize(depth);
+    p->recs_stage.resize(depth);
+    p->stat_stage.resize(depth);
+    p->framed.resize(depth);
+    p->opened.resize(depth);
     // The runtime spreads streams over a few hardware queues per priority, and a copy holds
     // its queue until it completes (kernels queued behind it wait; with the MAC stream
     // behind the H2D copies on one queue the call took 31.9 instead of 24.6 ms): the copy
@@ -644,6 +662,8 @@ int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, i
         TG_HIP(hipEventCreateWithFlags(&p->in_done[i], hipEventDisableTiming));
         TG_HIP(hipEventCreateWithFlags(&p->seal_done[i], hipEventDisableTiming));
         TG_HIP(hipEventCreateWithFlags(&p->out_done[i], hipEventDisableTiming));
+        TG_HIP(hipEventCreateWithFlags(&p->framed[i], hipEventDisableTiming));
+        TG_HIP(hipEventCreateWithFlags(&p->opened[i], hipEventDisableTiming));
     }
     *out = p;
     return 0;
@@ -657,14 +677,26 @@ int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p) {
     p->recs.release();
     p->chains.release();
     p->len.release();
+    for (DevBuf* b : {&p->rx, &p->opt, &p->conns, &p->rchains, &p->consumed, &p->fstatus, &p->totals}) b->release();
+    p->h_totals.release();
     for (int i = 0; i < p->depth; i++) {
         p->ws[i].release();
         p->pt_stage[i].release();
         p->wire_stage[i].release();
+        p->rrecs[i].release();
+        p->rstat[i].release();
+        p->rws[i].release();
+        p->fws[i].release();
+        p->rx_stage[i].release();
+        p->opt_stage[i].release();
+        p->recs_stage[i].release();
+        p->stat_stage[i].release();
         (void)hipEventDestroy(p->in_done[i]);
         (void)hipEventDestroy(p->seal_done[i]);
         (void)hipEventDestroy(p->out_done[i]);
         (void)hipEventDestroy(p->mac_done[i]);
+        (void)hipEventDestroy(p->framed[i]);
+        (void)hipEventDestroy(p->opened[i]);
     }
     for (hipStream_t s : {p->h2d, p->mac, p->cbc, p->d2h}) (void)hipStreamDestroy(s);
     delete p;
@@ -858,6 +890,251 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
     }
     // wire_len: ordered after every seal (each seal_done precedes its D2H copy, all drained)
     TG_HIP(hipMemcpy(wire_len_host, p->len.p, (size_t)nrecords * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// Receive path from host socket buffers (ABI 7): sub-batches of consecutive connections, about
+// p->chunk received bytes each, flow H2D copy (h2d stream) -> device framing -> open (one of
+// the two kernel streams, alternating per sub-batch) -> D2H of the opened plaintext, the framed
+// descriptors and the statuses (d2h stream), `depth` sub-batches in flight.  The open needs the
+// sub-batch's record count on the host (grids, workspace), so the host reads each framing's
+// total (4 bytes into pinned memory) before it enqueues that sub-batch's open: the wait falls
+// under the next sub-batch's H2D copy, which is enqueued first, so the copy engines -- the
+// bound of this path -- never wait for it.  A sub-batch's framing may use at most its share of
+// max_records (what the sub-batches before it left), so records are cut exactly where one
+// tlsgpu_frame_dev call over every connection would cut them.
+namespace {
+struct RxSub {
+    uint32_t c0, c1;   // connections [c0, c1)
+    size_t b0, b1;     // received bytes copied H2D, plaintext copied D2H: [b0, b1)
+    uint64_t bound;    // records its framing can produce at most (sum of span lengths / 5)
+};
+}  // namespace
+
+int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, size_t rx_bytes,
+                              const tlsgpu_span* conns, uint32_t n, uint32_t chain_flags, uint8_t* pt_host,
+                              size_t pt_bytes, tlsgpu_conn_state* states, uint32_t nstates, uint32_t variant,
+                              tlsgpu_open_record* records_host, uint32_t max_records, tlsgpu_chain* chains_host,
+                              uint32_t* consumed_host, int32_t* frame_status_host, int32_t* status_host,
+                              uint32_t* total_host) {
+    if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
+    if (!total_host) return fail(TLSGPU_EINVAL, "null pointer");
+    *total_host = 0;
+    if (n == 0) return 0;
+    if (!rx_host || !conns || !pt_host || !states || !chains_host || !consumed_host || !frame_status_host ||
+        (max_records && (!records_host || !status_host)))
+        return fail(TLSGPU_EINVAL, "null pointer");
+    if (n > (1u << 26)) return fail(TLSGPU_EINVAL, "too many connections");
+    if (pt_bytes < rx_bytes) return fail(TLSGPU_EINVAL, "plaintext arena smaller than the received bytes");
+    {
+        const uint32_t c = variant & 0xff, m = (variant >> 8) & 0xff;
+        const bool cbc = c == TLSGPU_CIPHER_AES128 || c == TLSGPU_CIPHER_AES256 || c == TLSGPU_CIPHER_3DES;
+        const bool ok = (cbc && m == TLSGPU_MAC_SHA1) || (cbc && c != TLSGPU_CIPHER_3DES && m == TLSGPU_MAC_SHA256) ||
+                        (c == TLSGPU_CIPHER_RC4 && (m == TLSGPU_MAC_SHA1 || m == TLSGPU_MAC_MD5));
+        if (!ok || (variant >> 17)) return fail(TLSGPU_EINVAL, "unsupported open variant");
+    }
+    // sub-batches of consecutive connections; spans outside the arena are refused by the
+    // framing (status EINVAL) and take no part in the copy ranges
+    std::vector<RxSub> sub;
+    {
+        RxSub cur = {0, 0, SIZE_MAX, 0, 0};
+        size_t acc = 0;
+        for (uint32_t c = 0; c < n; c++) {
+            const tlsgpu_span& sp = conns[c];
+            if (in_arena(sp.off, sp.len, rx_bytes) && sp.len) {
+                cur.b0 = sp.off < cur.b0 ? sp.off : cur.b0;
+                cur.b1 = sp.off + sp.len > cur.b1 ? sp.off + sp.len : cur.b1;
+                cur.bound += sp.len / 5;
+                acc += sp.len;
+            }
+            cur.c1 = c + 1;
+            if (acc >= p->chunk || c + 1 == n) {
+                if (cur.b0 == SIZE_MAX) cur.b0 = cur.b1 = 0;
+                sub.push_back(cur);
+                cur = {c + 1, c + 1, SIZE_MAX, 0, 0};
+                acc = 0;
+            }
+        }
+        // copy ranges must follow each other; otherwise everything is one sub-batch
+        bool mono = true;
+        size_t end = 0;
+        for (const RxSub& b : sub) {
+            if (b.b1 > b.b0 && b.b0 < end) mono = false;
+            end = b.b1 > end ? b.b1 : end;
+        }
+        if (!mono) {
+            RxSub all = {0, n, SIZE_MAX, 0, 0};
+            for (const RxSub& b : sub) {
+                if (b.b1 > b.b0) {
+                    all.b0 = b.b0 < all.b0 ? b.b0 : all.b0;
+                    all.b1 = b.b1 > all.b1 ? b.b1 : all.b1;
+                }
+                all.bound += b.bound;
+            }
+            if (all.b0 == SIZE_MAX) all.b0 = all.b1 = 0;
+            sub.assign(1, all);
+        }
+    }
+    const int D = p->depth;
+    const size_t nsub = sub.size();
+    const bool rx_direct = host_pinned(rx_host), pt_direct = host_pinned(pt_host);
+    const bool out_direct = max_records == 0 || (host_pinned(records_host) && host_pinned(status_host));
+    const bool need_ws = open_needs_workspace(variant);
+    uint64_t cap_max = 1, span_max = 0;
+    uint32_t nc_max = 1;
+    for (const RxSub& b : sub) {
+        const uint64_t c = b.bound + 1 < max_records ? b.bound + 1 : max_records;
+        cap_max = c > cap_max ? c : cap_max;
+        span_max = b.b1 - b.b0 > span_max ? b.b1 - b.b0 : span_max;
+        nc_max = b.c1 - b.c0 > nc_max ? b.c1 - b.c0 : nc_max;
+    }
+    TG_HIP(p->rx.ensure(rx_bytes));
+    TG_HIP(p->opt.ensure(rx_bytes));
+    TG_HIP(p->conns.ensure((size_t)n * sizeof(tlsgpu_span)));
+    TG_HIP(p->rchains.ensure((size_t)n * sizeof(tlsgpu_chain)));
+    TG_HIP(p->consumed.ensure((size_t)n * 4));
+    TG_HIP(p->fstatus.ensure((size_t)n * 4));
+    TG_HIP(p->totals.ensure((size_t)D * 4));
+    TG_HIP(p->h_totals.ensure((size_t)D * 4));
+    for (int t = 0; t < D; t++) {
+        TG_HIP(p->rrecs[t].ensure(cap_max * sizeof(tlsgpu_open_record)));
+        TG_HIP(p->rstat[t].ensure(cap_max * 4));
+        if (need_ws) TG_HIP(p->rws[t].ensure(open_workspace_bytes((uint32_t)cap_max)));
+        TG_HIP(p->fws[t].ensure(frame_workspace_bytes(nc_max)));
+        if (!rx_direct) TG_HIP(p->rx_stage[t].ensure(span_max));
+        if (!pt_direct) TG_HIP(p->opt_stage[t].ensure(span_max));
+    }
+    // the D2H ranges come back zero outside the opened bodies, never bytes of an earlier call
+    TG_HIP(hipMemsetAsync(p->opt.p, 0, rx_bytes, p->h2d));
+    TG_HIP(hipMemcpyAsync(p->conns.p, conns, (size_t)n * sizeof(tlsgpu_span), hipMemcpyHostToDevice, p->h2d));
+    const tlsgpu_span* d_conns = static_cast<const tlsgpu_span*>(p->conns.p);
+    tlsgpu_chain* d_chains = static_cast<tlsgpu_chain*>(p->rchains.p);
+    uint32_t* d_tot = static_cast<uint32_t*>(p->totals.p);
+    volatile uint32_t* h_tot = static_cast<volatile uint32_t*>(p->h_totals.p);
+    std::vector<uint32_t> base(nsub, 0), tot(nsub, 0);
+    uint32_t running = 0;
+    auto kstream = [&](size_t i) { return (i & 1) ? p->cbc : p->mac; };
+    // H2D of sub-batch i's received bytes (pageable: through slot t's pinned stage, whose
+    // previous copy -- sub-batch i - D's, drained by unstage before -- is done)
+    auto in_enq = [&](size_t i) -> int {
+        const RxSub& b = sub[i];
+        const int t = (int)(i % D);
+        if (b.b1 > b.b0) {
+            const uint8_t* src = rx_host + b.b0;
+            if (!rx_direct) {
+                stage_copy(p->rx_stage[t].u8(), src, b.b1 - b.b0);
+                src = p->rx_stage[t].u8();
+            }
+            TG_HIP(hipMemcpyAsync(p->rx.u8() + b.b0, src, b.b1 - b.b0, hipMemcpyHostToDevice, p->h2d));
+        }
+        TG_HIP(hipEventRecord(p->in_done[t], p->h2d));
+        return 0;
+    };
+    // framing of sub-batch i into slot t (after its bytes arrived and slot t's previous
+    // outputs left), its record count to pinned host memory
+    auto frame_enq = [&](size_t i) -> int {
+        const RxSub& b = sub[i];
+        const int t = (int)(i % D);
+        hipStream_t ks = kstream(i);
+        TG_HIP(hipStreamWaitEvent(ks, p->in_done[t], 0));
+        if (i >= (size_t)D) TG_HIP(hipStreamWaitEvent(ks, p->out_done[t], 0));
+        const uint64_t left = (uint64_t)max_records - running;
+        const uint32_t cap = (uint32_t)(b.bound + 1 < left ? b.bound + 1 : left);
+        hipError_t e = launch_frame(p->rx.u8(), rx_bytes, d_conns + b.c0, b.c1 - b.c0,
+                                    static_cast<tlsgpu_open_record*>(p->rrecs[t].p), cap, d_chains + b.c0,
+                                    chain_flags, static_cast<uint32_t*>(p->consumed.p) + b.c0,
+                                    static_cast<int32_t*>(p->fstatus.p) + b.c0, d_tot + t, p->fws[t].u8(), ks);
+        if (e != hipSuccess) return fail_hip(e, "host pipeline framing");
+        TG_HIP(hipMemcpyAsync((void*)(h_tot + t), d_tot + t, 4, hipMemcpyDeviceToHost, ks));
+        TG_HIP(hipEventRecord(p->framed[t], ks));
+        return 0;
+    };
+    // open of sub-batch i once its count is known, then its D2H copies
+    auto finish = [&](size_t i) -> int {
+        const RxSub& b = sub[i];
+        const int t = (int)(i % D);
+        hipStream_t ks = kstream(i);
+        TG_HIP(hipEventSynchronize(p->framed[t]));
+        const uint32_t T = h_tot[t];
+        tot[i] = T;
+        base[i] = running;
+        running += T;
+        if (T) {
+            Bounds ob;
+            ob.wire_cap = rx_bytes;
+            ob.pt_cap = rx_bytes;
+            ob.nstates = nstates;
+            bool known = false;
+            hipError_t e = launch_open(variant, d_chains + b.c0, b.c1 - b.c0,
+                                       static_cast<const tlsgpu_open_record*>(p->rrecs[t].p), T, p->rx.u8(),
+                                       p->opt.u8(), S(states), static_cast<int32_t*>(p->rstat[t].p), p->rws[t].u8(),
+                                       next_epoch(), ks, &known, ob);
+            if (!known) return fail(TLSGPU_EINVAL, "unsupported open variant");
+            if (e != hipSuccess) return fail_hip(e, "host pipeline open");
+        }
+        TG_HIP(hipEventRecord(p->opened[t], ks));
+        TG_HIP(hipStreamWaitEvent(p->d2h, p->opened[t], 0));
+        if (b.b1 > b.b0) {
+            uint8_t* dst = pt_direct ? pt_host + b.b0 : p->opt_stage[t].u8();
+            TG_HIP(hipMemcpyAsync(dst, p->opt.u8() + b.b0, b.b1 - b.b0, hipMemcpyDeviceToHost, p->d2h));
+        }
+        if (T) {
+            void* rd = records_host + base[i];
+            void* sd = status_host + base[i];
+            if (!out_direct) {
+                TG_HIP(p->recs_stage[t].ensure((size_t)T * sizeof(tlsgpu_open_record)));
+                TG_HIP(p->stat_stage[t].ensure((size_t)T * 4));
+                rd = p->recs_stage[t].p;
+                sd = p->stat_stage[t].p;
+            }
+            TG_HIP(hipMemcpyAsync(rd, p->rrecs[t].p, (size_t)T * sizeof(tlsgpu_open_record), hipMemcpyDeviceToHost,
+                                  p->d2h));
+            TG_HIP(hipMemcpyAsync(sd, p->rstat[t].p, (size_t)T * 4, hipMemcpyDeviceToHost, p->d2h));
+        }
+        TG_HIP(hipEventRecord(p->out_done[t], p->d2h));
+        return 0;
+    };
+    // sub-batch j's staged outputs to the caller's arrays (after its D2H copies)
+    auto unstage = [&](size_t j) -> int {
+        const int t = (int)(j % D);
+        TG_HIP(hipEventSynchronize(p->out_done[t]));
+        if (!pt_direct && sub[j].b1 > sub[j].b0)
+            stage_copy(pt_host + sub[j].b0, p->opt_stage[t].u8(), sub[j].b1 - sub[j].b0);
+        if (!out_direct && tot[j]) {
+            memcpy(records_host + base[j], p->recs_stage[t].p, (size_t)tot[j] * sizeof(tlsgpu_open_record));
+            memcpy(status_host + base[j], p->stat_stage[t].p, (size_t)tot[j] * 4);
+        }
+        return 0;
+    };
+    const bool staged = !rx_direct || !pt_direct || !out_direct;
+    for (size_t i = 0; i < nsub; i++) {
+        int rc;
+        // with one slot, sub-batch i - 1 must be opened and copied out before i reuses the slot
+        if (D == 1 && i >= 1 && (rc = finish(i - 1))) return rc;
+        if (staged && i >= (size_t)D && (rc = unstage(i - D))) return rc;  // slot t's stages free again
+        if ((rc = in_enq(i))) return rc;
+        // the wait for sub-batch i - 1's count falls under sub-batch i's H2D copy
+        if (D > 1 && i >= 1 && (rc = finish(i - 1))) return rc;
+        if ((rc = frame_enq(i))) return rc;
+    }
+    {
+        int rc = finish(nsub - 1);
+        if (rc) return rc;
+    }
+    TG_HIP(hipStreamSynchronize(p->d2h));
+    if (staged)
+        for (size_t j = nsub > (size_t)D ? nsub - D : 0; j < nsub; j++) {
+            int rc = unstage(j);
+            if (rc) return rc;
+        }
+    // per-connection results (every framing is done: each open waited for its framing, and
+    // the d2h stream for each open)
+    TG_HIP(hipMemcpy(chains_host, d_chains, (size_t)n * sizeof(tlsgpu_chain), hipMemcpyDeviceToHost));
+    TG_HIP(hipMemcpy(consumed_host, p->consumed.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    TG_HIP(hipMemcpy(frame_status_host, p->fstatus.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < nsub; i++)
+        for (uint32_t c = sub[i].c0; c < sub[i].c1; c++) chains_host[c].first += base[i];
+    *total_host = running;
     return 0;
 }
 

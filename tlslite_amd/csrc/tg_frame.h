@@ -28,7 +28,8 @@ struct FrameWalk {
 // descriptors.  The checks in the reference's order: the first byte of a header must be a
 // content type as soon as it arrives (:850-857, SyntaxError otherwise -- an SSLv2 header, 128,
 // belongs to the handshake), then the 5-byte header, its length against 18432 (:871-873), then
-// the body must be complete.
+// the body: an empty one ends the connection (the body loop's sock.recv(0) returns b"" and
+// raises TLSAbruptCloseError, :877-889; ABI 7), else it must be complete.
 __device__ __forceinline__ FrameWalk frame_walk(const uint8_t* __restrict__ s, uint64_t off, uint64_t len,
                                                 uint32_t limit, tlsgpu_open_record* __restrict__ out) {
     uint64_t pos = off;
@@ -45,6 +46,10 @@ __device__ __forceinline__ FrameWalk frame_walk(const uint8_t* __restrict__ s, u
         const uint32_t L = ((uint32_t)s[pos + 3] << 8) | s[pos + 4];
         if (L > FRAME_MAX_BODY) {
             code = TLSGPU_ALERT_RECORD_OVERFLOW;
+            break;
+        }
+        if (L == 0) {
+            code = TLSGPU_EABRUPT;
             break;
         }
         if (end - pos - 5 < L) break;  // body incomplete
@@ -66,8 +71,9 @@ __device__ __forceinline__ FrameWalk frame_walk(const uint8_t* __restrict__ s, u
 __global__ void __launch_bounds__(FRAME_BLOCK) frame_count_kernel(const uint8_t* __restrict__ s, uint64_t cap,
                                                                  const tlsgpu_span* __restrict__ conns, uint32_t n,
                                                                  uint32_t* __restrict__ counts,
-                                                                 uint32_t* __restrict__ block_sums) {
-    __shared__ uint32_t red[FRAME_BLOCK / 64];
+                                                                 uint64_t* __restrict__ block_sums) {
+    // 64-bit sums: 256 connections' spans may overlap and frame more than 2^32 records
+    __shared__ uint64_t red[FRAME_BLOCK / 64];
     const uint32_t i = blockIdx.x * FRAME_BLOCK + threadIdx.x;
     uint32_t c = 0;
     if (i < n) {
@@ -75,13 +81,13 @@ __global__ void __launch_bounds__(FRAME_BLOCK) frame_count_kernel(const uint8_t*
         if (in_arena(sp.off, sp.len, cap)) c = frame_walk(s, sp.off, sp.len, 0xffffffffu, nullptr).count;
         counts[i] = c;
     }
-    uint32_t w = c;
+    uint64_t w = c;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) w += (uint32_t)__shfl_xor((int)w, o);
+    for (int o = 1; o < 64; o <<= 1) w += (uint64_t)__shfl_xor((unsigned long long)w, o);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t = 0;
+        uint64_t t = 0;
 #pragma unroll
         for (int k = 0; k < FRAME_BLOCK / 64; k++) t += red[k];
         block_sums[blockIdx.x] = t;
@@ -90,7 +96,7 @@ __global__ void __launch_bounds__(FRAME_BLOCK) frame_count_kernel(const uint8_t*
 
 // exclusive scan of nb block totals in place (one block of 1024 threads, each a contiguous
 // piece), the grand total to *total (64-bit sums: 2^26 connections of up to 2^32 records)
-__global__ void __launch_bounds__(1024) frame_scan_kernel(uint32_t* __restrict__ block_sums, uint32_t nb,
+__global__ void __launch_bounds__(1024) frame_scan_kernel(uint64_t* __restrict__ block_sums, uint32_t nb,
                                                         uint32_t* __restrict__ total, uint32_t max_records) {
     __shared__ uint64_t part[1024];
     const uint32_t per = (nb + 1023) / 1024, a = threadIdx.x * per, b = min(nb, a + per);
@@ -110,34 +116,34 @@ __global__ void __launch_bounds__(1024) frame_scan_kernel(uint32_t* __restrict__
     __syncthreads();
     uint64_t run = part[threadIdx.x];
     for (uint32_t k = a; k < b; k++) {
-        const uint32_t v = block_sums[k];
-        block_sums[k] = (uint32_t)min<uint64_t>(run, 0xffffffffu);
+        const uint64_t v = block_sums[k];
+        block_sums[k] = run;
         run += v;
     }
 }
 
 __global__ void __launch_bounds__(FRAME_BLOCK) frame_write_kernel(
     const uint8_t* __restrict__ s, uint64_t cap, const tlsgpu_span* __restrict__ conns, uint32_t n,
-    const uint32_t* __restrict__ counts, const uint32_t* __restrict__ block_off, tlsgpu_open_record* __restrict__ recs,
+    const uint32_t* __restrict__ counts, const uint64_t* __restrict__ block_off, tlsgpu_open_record* __restrict__ recs,
     uint32_t max_records, tlsgpu_chain* __restrict__ chains, uint32_t chain_flags, uint32_t* __restrict__ consumed,
     int32_t* __restrict__ status) {
-    __shared__ uint32_t wsum[FRAME_BLOCK / 64];
+    __shared__ uint64_t wsum[FRAME_BLOCK / 64];
     const uint32_t i = blockIdx.x * FRAME_BLOCK + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t c = i < n ? counts[i] : 0u;
     // inclusive scan of c over the wave, then over the block's waves
-    uint32_t x = c;
+    uint64_t x = c;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        const uint64_t y = (uint64_t)__shfl_up((unsigned long long)x, o);
         if (lane >= (uint32_t)o) x += y;
     }
     if (lane == 63) wsum[wv] = x;
     __syncthreads();
-    uint32_t before = 0;
+    uint64_t before = 0;
     for (uint32_t k = 0; k < wv; k++) before += wsum[k];
     if (i >= n) return;
-    const uint64_t first = (uint64_t)block_off[blockIdx.x] + before + (x - c);
+    const uint64_t first = block_off[blockIdx.x] + before + (x - c);
     const tlsgpu_span sp = conns[i];
     tlsgpu_chain ch;
     ch.state = sp.state;

@@ -868,15 +868,16 @@ hipError_t launch_open(uint32_t variant, const tlsgpu_chain* chains, uint32_t nc
 
 
 // ---------------------------------------------------------------- receive framing
+// per connection its record count (uint32), then per block of connections its 64-bit sum
 size_t frame_workspace_bytes(uint32_t n) {
-    return (size_t)n * 4 + (size_t)((n + FRAME_BLOCK - 1) / FRAME_BLOCK) * 4 + 16;
+    return (((size_t)n * 4 + 7) & ~(size_t)7) + (size_t)((n + FRAME_BLOCK - 1) / FRAME_BLOCK) * 8 + 16;
 }
 hipError_t launch_frame(const uint8_t* stream, uint64_t cap, const tlsgpu_span* conns, uint32_t n,
                         tlsgpu_open_record* recs, uint32_t max_records, tlsgpu_chain* chains, uint32_t chain_flags,
                         uint32_t* consumed, int32_t* status, uint32_t* total, uint8_t* ws, hipStream_t s) {
     const uint32_t nb = (n + FRAME_BLOCK - 1) / FRAME_BLOCK;
     uint32_t* counts = reinterpret_cast<uint32_t*>(ws);
-    uint32_t* bsum = counts + n;
+    uint64_t* bsum = reinterpret_cast<uint64_t*>(ws + (((size_t)n * 4 + 7) & ~(size_t)7));
     hipLaunchKernelGGL(frame_count_kernel, dim3(nb), dim3(FRAME_BLOCK), 0, s, stream, cap, conns, n, counts, bsum);
     hipLaunchKernelGGL(frame_scan_kernel, dim3(1), dim3(1024), 0, s, bsum, nb, total, max_records);
     hipLaunchKernelGGL(frame_write_kernel, dim3(nb), dim3(FRAME_BLOCK), 0, s, stream, cap, conns, n, counts, bsum,

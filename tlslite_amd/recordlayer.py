@@ -33,6 +33,11 @@ class RecordSyntaxError(SyntaxError):
     (tlsrecordlayer.py:850-857 raises SyntaxError)."""
 
 
+class RecordAbruptClose(ConnectionError):
+    """A record header announced an empty body: the reference's body loop calls
+    sock.recv(0), gets b"" and raises TLSAbruptCloseError (tlsrecordlayer.py:877-889)."""
+
+
 class BadRecordMAC(ValueError):
     """bad_record_mac alert (tlsrecordlayer.py:1039-1042)."""
 
@@ -58,6 +63,8 @@ def parse_records(data):
         length = (data[pos + 3] << 8) | data[pos + 4]
         if length > MAX_RECORD_BODY:
             raise RecordOverflow("record length %d > %d" % (length, MAX_RECORD_BODY))
+        if length == 0:
+            raise RecordAbruptClose("empty record body (recv(0) in the reference)")
         if len(data) - pos - 5 < length:
             break
         out.append((ctype, (vmaj, vmin), data[pos + 5:pos + 5 + length]))
@@ -202,12 +209,12 @@ class SealPipeline:
 
 
 class HostSealPipeline:
-    """Seal batches whose plaintext and wire arenas live in HOST memory
-    (tlsgpu_host_pipeline_*): the records' socket-buffer hand-off
-    (tlsrecordlayer.py:616-620) with H2D copy, seal and D2H copy of successive
-    sub-batches overlapped on `depth` streams.  Pinned host arrays
-    (device.PinnedBuffer) are copied directly, pageable ones through
-    library-owned pinned staging buffers."""
+    """Seal and open batches whose arenas live in HOST memory (tlsgpu_host_pipeline_*):
+    seal -- the records' socket-buffer hand-off (tlsrecordlayer.py:616-620) with H2D copy,
+    seal and D2H copy of successive sub-batches overlapped on `depth` streams; open -- the
+    receive path from socket buffers (:832-893, :958-1044): H2D copy, framing and open on the
+    device, D2H copy of the plaintext.  Pinned host arrays (device.PinnedBuffer) are copied
+    directly, pageable ones through library-owned pinned staging buffers."""
 
     def __init__(self, chunk_bytes=64 << 20, depth=3):
         h = ctypes.c_void_p()
@@ -221,6 +228,40 @@ class HostSealPipeline:
                ctypes.addressof(records), len(records), pt_host.ctypes.data_as(ctypes.c_void_p), pt_host.nbytes,
                wire_host.ctypes.data_as(ctypes.c_void_p), wire_host.nbytes, states.ptr, _nstates(states, nstates),
                wire_len_host.ctypes.data_as(ctypes.c_void_p), variant)
+
+    def open(self, rx_host, spans, pt_host, states, variant, max_records=None, chain_flags=None, nstates=None,
+             out=None):
+        """Open the records in connections' received bytes (tlsgpu_host_pipeline_open).
+        rx_host: numpy uint8 (host) holding every connection's bytes; spans: ctypes array of
+        N.Span {off, len, state}; pt_host: numpy uint8 (host, >= rx_host.nbytes) for the
+        opened bodies; states: DeviceBuffer of read states.  max_records None: every record
+        the bytes can hold.  out: optional dict of preallocated host arrays (records /
+        status: pinned ones are copied to directly).  Returns a dict: records (ctypes
+        N.OpenRecord array), status (int32), chains (N.Chain array), consumed (uint32),
+        frame_status (int32), total."""
+        n = len(spans)
+        flags = N.CHAIN_STOP_ON_ALERT if chain_flags is None else int(chain_flags)
+        if max_records is None:
+            max_records = sum(int(sp.len) // 5 for sp in spans) + 1
+        out = dict(out or {})
+        recs = out.get("records")
+        if recs is None:
+            recs = (N.OpenRecord * max(1, max_records))()
+        status = out.get("status")
+        if status is None:
+            status = np.zeros(max(1, max_records), dtype=np.int32)
+        chains = (N.Chain * n)()
+        consumed = np.zeros(n, dtype=np.uint32)
+        fstatus = np.zeros(n, dtype=np.int32)
+        total = ctypes.c_uint32()
+        rp = recs.ctypes.data_as(ctypes.c_void_p) if isinstance(recs, np.ndarray) else ctypes.addressof(recs)
+        N.call("tlsgpu_host_pipeline_open", self.handle, rx_host.ctypes.data_as(ctypes.c_void_p), rx_host.nbytes,
+               ctypes.addressof(spans), n, flags, pt_host.ctypes.data_as(ctypes.c_void_p), pt_host.nbytes,
+               states.ptr, _nstates(states, nstates), variant, rp, int(max_records), ctypes.addressof(chains),
+               consumed.ctypes.data_as(ctypes.c_void_p), fstatus.ctypes.data_as(ctypes.c_void_p),
+               status.ctypes.data_as(ctypes.c_void_p), ctypes.byref(total))
+        return {"records": recs, "status": status[: total.value], "chains": chains, "consumed": consumed,
+                "frame_status": fstatus, "total": total.value}
 
     def close(self):
         if self.handle is not None and self.handle.value:
