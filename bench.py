@@ -315,9 +315,9 @@ def pcie_rates(nbytes=256 << 20):
     hip.hipStreamCreateWithFlags(ctypes.byref(s2), 1)
     hip.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
     res = {}
-    for name, mode in (("h2d", 1), ("d2h", 2), ("both", 3)):
+    for name, mode in (("warm", 3), ("h2d", 1), ("d2h", 2), ("both", 3)):  # "warm": untimed first copies
         best = None
-        for _ in range(4):
+        for _ in range(6 if name != "warm" else 2):
             hip.hipDeviceSynchronize()
             t0 = time.perf_counter()
             if mode & 1:
@@ -328,7 +328,8 @@ def pcie_rates(nbytes=256 << 20):
             hip.hipStreamSynchronize(s2)
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
-        res[name] = round(nbytes * (2 if mode == 3 else 1) / best / 1e9, 1)
+        if name != "warm":
+            res[name] = round(nbytes * (2 if mode == 3 else 1) / best / 1e9, 1)
     for ptr in (h1, h2):
         hip.hipHostFree(ptr)
     for ptr in (d1, d2):

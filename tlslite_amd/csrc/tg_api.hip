@@ -608,6 +608,7 @@ struct tlsgpu_host_pipeline_s {
     int depth = 2;
     size_t chunk = 0;
     hipStream_t h2d = nullptr, mac = nullptr, cbc = nullptr, d2h = nullptr;
+    hipStream_t frs = nullptr;  // receive framing: its own (high-priority) queue, never behind an open
     std::vector<hipEvent_t> mac_done;
     std::vector<hipEvent_t> in_done, seal_done, out_done;
     DevBuf pt, wire, recs, chains, len;
@@ -621,6 +622,7 @@ struct tlsgpu_host_pipeline_s {
     std::vector<PinBuf> rx_stage, opt_stage, recs_stage, stat_stage;
     PinBuf h_totals;
     std::vector<hipEvent_t> framed, opened;
+    std::vector<hipEvent_t> rx_in;  // per sub-batch of a receive call: its H2D copy is done
 };
 
 int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, int depth) {
@@ -655,6 +657,7 @@ int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, i
     TG_HIP(hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio));
     TG_HIP(hipStreamCreateWithPriority(&p->h2d, hipStreamNonBlocking, hi_prio));
     TG_HIP(hipStreamCreateWithPriority(&p->d2h, hipStreamNonBlocking, hi_prio));
+    TG_HIP(hipStreamCreateWithPriority(&p->frs, hipStreamNonBlocking, hi_prio));
     TG_HIP(hipStreamCreateWithFlags(&p->mac, hipStreamNonBlocking));
     TG_HIP(hipStreamCreateWithFlags(&p->cbc, hipStreamNonBlocking));
     for (int i = 0; i < depth; i++) {
@@ -671,7 +674,7 @@ int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, i
 
 int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p) {
     if (!p) return 0;
-    for (hipStream_t s : {p->h2d, p->mac, p->cbc, p->d2h}) (void)hipStreamSynchronize(s);
+    for (hipStream_t s : {p->h2d, p->mac, p->cbc, p->d2h, p->frs}) (void)hipStreamSynchronize(s);
     p->pt.release();
     p->wire.release();
     p->recs.release();
@@ -698,7 +701,8 @@ int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p) {
         (void)hipEventDestroy(p->framed[i]);
         (void)hipEventDestroy(p->opened[i]);
     }
-    for (hipStream_t s : {p->h2d, p->mac, p->cbc, p->d2h}) (void)hipStreamDestroy(s);
+    for (hipEvent_t e : p->rx_in) (void)hipEventDestroy(e);
+    for (hipStream_t s : {p->h2d, p->mac, p->cbc, p->d2h, p->frs}) (void)hipStreamDestroy(s);
     delete p;
     return 0;
 }
@@ -995,6 +999,11 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
     TG_HIP(p->consumed.ensure((size_t)n * 4));
     TG_HIP(p->fstatus.ensure((size_t)n * 4));
     TG_HIP(p->totals.ensure((size_t)D * 4));
+    while (p->rx_in.size() < nsub) {
+        hipEvent_t e = nullptr;
+        TG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        p->rx_in.push_back(e);
+    }
     TG_HIP(p->h_totals.ensure((size_t)D * 4));
     for (int t = 0; t < D; t++) {
         TG_HIP(p->rrecs[t].ensure(cap_max * sizeof(tlsgpu_open_record)));
@@ -1027,7 +1036,7 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
             }
             TG_HIP(hipMemcpyAsync(p->rx.u8() + b.b0, src, b.b1 - b.b0, hipMemcpyHostToDevice, p->h2d));
         }
-        TG_HIP(hipEventRecord(p->in_done[t], p->h2d));
+        TG_HIP(hipEventRecord(p->rx_in[i], p->h2d));
         return 0;
     };
     // framing of sub-batch i into slot t (after its bytes arrived and slot t's previous
@@ -1035,8 +1044,8 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
     auto frame_enq = [&](size_t i) -> int {
         const RxSub& b = sub[i];
         const int t = (int)(i % D);
-        hipStream_t ks = kstream(i);
-        TG_HIP(hipStreamWaitEvent(ks, p->in_done[t], 0));
+        hipStream_t ks = p->frs;
+        TG_HIP(hipStreamWaitEvent(ks, p->rx_in[i], 0));
         if (i >= (size_t)D) TG_HIP(hipStreamWaitEvent(ks, p->out_done[t], 0));
         const uint64_t left = (uint64_t)max_records - running;
         const uint32_t cap = (uint32_t)(b.bound + 1 < left ? b.bound + 1 : left);
@@ -1059,6 +1068,7 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
         tot[i] = T;
         base[i] = running;
         running += T;
+        TG_HIP(hipStreamWaitEvent(ks, p->framed[t], 0));
         if (T) {
             Bounds ob;
             ob.wire_cap = rx_bytes;
@@ -1106,15 +1116,30 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
         }
         return 0;
     };
-    const bool staged = !rx_direct || !pt_direct || !out_direct;
+    // H2D copies run ahead of the framing: pinned received bytes are all enqueued at once (each
+    // sub-batch has its own device range and event); pageable ones one sub-batch ahead, as far
+    // as the pinned stages allow (slot (i + 1) % D's previous copy, i + 1 - D's, is done once
+    // sub-batch i - 1's framing has been seen).
+    const bool staged = !pt_direct || !out_direct;
+    size_t issued = 0;
+    auto issue_upto = [&](size_t lim) -> int {
+        for (; issued < lim && issued < nsub; issued++) {
+            int rc = in_enq(issued);
+            if (rc) return rc;
+        }
+        return 0;
+    };
+    {
+        int rc = issue_upto(rx_direct ? nsub : 1);
+        if (rc) return rc;
+    }
     for (size_t i = 0; i < nsub; i++) {
         int rc;
-        // with one slot, sub-batch i - 1 must be opened and copied out before i reuses the slot
-        if (D == 1 && i >= 1 && (rc = finish(i - 1))) return rc;
+        // sub-batch i - 1's count: the wait falls under sub-batch i's H2D copy, already queued
+        // (with one slot, i - 1 must also be copied out before i reuses the slot)
+        if (i >= 1 && (rc = finish(i - 1))) return rc;
         if (staged && i >= (size_t)D && (rc = unstage(i - D))) return rc;  // slot t's stages free again
-        if ((rc = in_enq(i))) return rc;
-        // the wait for sub-batch i - 1's count falls under sub-batch i's H2D copy
-        if (D > 1 && i >= 1 && (rc = finish(i - 1))) return rc;
+        if (!rx_direct && (rc = issue_upto(D == 1 ? i + 1 : i + 2))) return rc;
         if ((rc = frame_enq(i))) return rc;
     }
     {

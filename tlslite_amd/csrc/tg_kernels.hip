@@ -765,9 +765,19 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
         hipLaunchKernelGGL((open_seq_kernel<MAC, SSL3>), dim3((c1 - c0 + 255) / 256), dim3(256), 0, s, chains, nchains,
                            recs, nrecords, pt, states, status, meta, epoch, c0, c1, b.nstates);
     };
+    // At most one wave of records per CU (the receive pipeline's sub-batches): the MAC is
+    // latency-bound -- cooperative loads, and one wave per workgroup so the waves spread over
+    // as many CUs as there are waves (four 256-lane workgroups put a 1,024-record batch on 4
+    // CUs, where the concurrent sub-batches' MAC and framing kernels land too: 1.4 ms in the
+    // pipeline against 0.35 ms alone, tools/open_mac_probe.py)
+    const bool coop = nrecords <= 64u * ncu;
     auto mac = [&](uint32_t c0, uint32_t c1, hipStream_t s, int part = -1, int nparts = 0) {
-        hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3, BS>), gr, dim3(256), 0, s, recs, nrecords, pt, states, status,
-                           meta, ms, epoch, c0, c1, part, nparts);
+        if (coop)
+            hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3, BS, true>), dim3((nrecords + 63) / 64), dim3(64), 0, s, recs,
+                               nrecords, pt, states, status, meta, ms, epoch, c0, c1, part, nparts);
+        else
+            hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3, BS, false>), gr, dim3(256), 0, s, recs, nrecords, pt,
+                               states, status, meta, ms, epoch, c0, c1, part, nparts);
     };
     // Chain-range parts only when each part's MAC pass alone holds two waves per SIMD (one lane
     // per record: with fewer records a part's MAC takes as long as the whole batch's, and four

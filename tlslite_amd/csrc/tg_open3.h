@@ -567,7 +567,13 @@ __device__ __forceinline__ uint32_t open_chunks_ready(uint32_t nb, uint32_t E, u
     return min(nfull, bytes >> 6);
 }
 
-template <int MAC, bool SSL3, int BS>
+// COOP (round 6): a batch of at most one record per lane of one wave per CU (the receive
+// pipeline's 64 MiB sub-batches of 16 KiB records: 4,096 lanes on 256 CUs) is latency-bound,
+// and with per-lane 64-B loads one chunk ahead every compression waited for its load (1.3 ms
+// for 256 compressions against the seal MAC's 0.34 ms); there the quad-cooperative loads with
+// the seal's two-chunk ring (mac_bulk_coop) feed the lanes.  Large batches keep the per-lane
+// loads (round 4: the cooperative form measured 1-2 % slower on cfg2 / cfg3).
+template <int MAC, bool SSL3, int BS, bool COOP>
 __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record* __restrict__ recs, uint32_t nrecords,
                                                       const uint8_t* __restrict__ pt,
                                                       const ConnState* __restrict__ states,
@@ -579,34 +585,61 @@ __global__ void __launch_bounds__(256) open_mac_kernel(const tlsgpu_open_record*
     constexpr int DL = M::DL;
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     // the chain first: records of other parts may be in their padding pass right now
-    if (r >= nrecords || meta[r].chain - c_lo >= c_hi - c_lo) return;
-    const OpenMeta mt = meta[r];
-    if (mt.epoch != epoch || !(mt.flags & OM_VERIFY)) return;
-    const ConnState* st = states + mt.state;
-    const tlsgpu_open_record R = recs[r];
-    const uint8_t* P = pt + R.pt_off;
-    const uint32_t n = mt.n;
-    const uint32_t nfull = n >> 6;
-    M mac;
-    uint32_t c0 = 0, c1 = nfull;
-    if (part >= 0) {
-        const uint32_t E = st->explicit_iv ? (uint32_t)BS : 0u;
-        const uint32_t nb = R.ct_len / BS;
-        c0 = part == 0 ? 0u : open_chunks_ready<BS>(nb, E, nfull, part - 1, nparts);
-        c1 = part == nparts ? nfull : open_chunks_ready<BS>(nb, E, nfull, part, nparts);
+    bool act = r < nrecords && meta[r].chain - c_lo < c_hi - c_lo;
+    OpenMeta mt = {};
+    if (act) {
+        mt = meta[r];
+        act = mt.epoch == epoch && (mt.flags & OM_VERIFY);
     }
-    if (c0 == 0) {
-        mac.begin(st, mt.seq, R.content_type, n);
-    } else {
-        const OpenMacState& q = ms[r];
+    if constexpr (!COOP) {
+        if (!act) return;
+    }
+    // no early exit before the bulk in the cooperative form: the quad exchanges loaded data (DPP)
+    const ConnState* st = states;
+    tlsgpu_open_record R = {};
+    const uint8_t* P = pt;
+    uint32_t n = 0, nfull = 0, c0 = 0, c1 = 0;
+    M mac;
+    if (act) {
+        st = states + mt.state;
+        R = recs[r];
+        P = pt + R.pt_off;
+        n = mt.n;
+        nfull = n >> 6;
+        c1 = nfull;
+        if (part >= 0) {
+            const uint32_t E = st->explicit_iv ? (uint32_t)BS : 0u;
+            const uint32_t nb = R.ct_len / BS;
+            c0 = part == 0 ? 0u : open_chunks_ready<BS>(nb, E, nfull, part - 1, nparts);
+            c1 = part == nparts ? nfull : open_chunks_ready<BS>(nb, E, nfull, part, nparts);
+        }
+        if (c0 == 0) {
+            mac.begin(st, mt.seq, R.content_type, n);
+        } else {
+            const OpenMacState& q = ms[r];
 #pragma unroll
-        for (int k = 0; k < 8; k++) mac.h[k] = q.h[k];
+            for (int k = 0; k < 8; k++) mac.h[k] = q.h[k];
 #pragma unroll
-        for (int k = 0; k < 4; k++) mac.prev[k] = q.prev[k];
+            for (int k = 0; k < 4; k++) mac.prev[k] = q.prev[k];
+        }
     }
     const uint8_t* Pc = P + 64 * c0;
-    if (((uintptr_t)P & 15) == 0) mac_bulk<true>(mac, Pc, c1 - c0);
-    else mac_bulk<false>(mac, Pc, c1 - c0);
+    const bool al16 = ((uintptr_t)P & 15) == 0;
+    if constexpr (COOP) {
+        uint32_t coop = (act && al16 && c1 > c0) ? 1u : 0u;
+        coop &= quad_dpp<0xB1>(coop);
+        coop &= quad_dpp<0x4E>(coop);
+        if (coop) {
+            mac_bulk_coop<MAC_PF>(mac, Pc, c1 - c0, threadIdx.x & 3u);
+        } else if (act) {
+            if (al16) mac_bulk<true>(mac, Pc, c1 - c0);
+            else mac_bulk<false>(mac, Pc, c1 - c0);
+        }
+        if (!act) return;
+    } else {
+        if (al16) mac_bulk<true>(mac, Pc, c1 - c0);
+        else mac_bulk<false>(mac, Pc, c1 - c0);
+    }
     if (part >= 0 && part < nparts) {  // more parts follow: keep the hash state
         OpenMacState& q = ms[r];
 #pragma unroll
