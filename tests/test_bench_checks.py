@@ -117,11 +117,13 @@ def test_open_leg_aggregated_over_ranks():
     assert bench.open_over_ranks(_FakeRanks([a, b2], [gib, gib]), a, gib)["roundtrip_exact"] is False
     r = bench.open_over_ranks(_FakeRanks([a, {"error": "boom"}], [gib, gib]), a, gib)
     assert "error" in r and "rank(s) [1]" in r["error"]
-    # with wall-clock-timed concurrent runs on every rank, those set the job's rate
+    # wall-clock-timed concurrent runs on every rank: aggregated beside the headline, which
+    # stays the per-call median as at N = 1 (one metric at every N)
     ac = dict(a, concurrent={"ms": 2.0, "roundtrip_exact": True})
     bc = dict(b, concurrent={"ms": 2.5, "roundtrip_exact": True})
     r = bench.open_over_ranks(_FakeRanks([ac, bc], [gib, gib]), ac, gib)
-    assert r["ms"] == 2.5 and r["value"] == round(2.0 / 0.0025, 2) and "wall time" in r["aggregate"]
+    assert r["ms"] == 1.3 and r["value"] == round(2.0 / (1.30 / 1e3), 2) and "median" in r["aggregate"]
+    assert r["concurrent_value"] == round(2.0 / 0.0025, 2) and "wall time" in r["concurrent_aggregate"]
     bc2 = dict(bc, concurrent={"ms": 2.5, "roundtrip_exact": False})
     assert bench.open_over_ranks(_FakeRanks([ac, bc2], [gib, gib]), ac, gib)["roundtrip_exact"] is False
 

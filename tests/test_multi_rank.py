@@ -94,8 +94,10 @@ from tlslite_amd.device import Stream, device_count, set_device, synchronize
 from tlslite_amd.recordlayer import SealPipeline, seal_dev
 from tlslite_amd.shard import ShardGroup, device_for_rank, shard_indices
 g = ShardGroup()
-# one GPU per rank (LOCAL_RANK % devices): distinct devices on a multi-GPU node, both
-# ranks on the one GPU of a single-GPU box (the per-device paths then still run twice)
+# one GPU per rank (LOCAL_RANK % devices): distinct devices on a multi-GPU node -- there rank 1
+# drives device 1 of the full device list (unlike bench.py, which narrows each rank's visible
+# devices to its own device 0), so this is a device != 0 run of the library, as are
+# tests/test_gpu_multidevice.py's -- and both ranks on the one GPU of a single-GPU box
 dev = device_for_rank(g.local, device_count())
 set_device(dev)
 print("DEVICE %d %d" % (g.rank, dev), file=sys.stderr)
