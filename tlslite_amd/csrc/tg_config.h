@@ -23,6 +23,10 @@ constexpr int CFG_MAC_LB = 3;
 // the many-chains MAC kernel (cfg3): <= 128 VGPRs, one-chunk prefetch
 constexpr int CFG_MAC_LB_MANY = 4;
 constexpr int CFG_MAC_PF_MANY = 1;
+// LDS bytes the many-chains MAC launch reserves per 256-thread workgroup: none (the kernel
+// uses no LDS).  Experiment builds set it to what an LDS staging of each record's current
+// 128-B plaintext line would take (8 KiB), to measure that occupancy cost alone (round 6).
+constexpr int CFG_MAC_MANY_LDS = 0;
 // cbc_pair_kernel: waves per CU in the many-chains regime; prefetch group (blocks) in the
 // one-generation (cfg2) and many-chains (cfg3) regimes
 constexpr int CFG_PAIR_WAVES_MANY = 8;

@@ -422,8 +422,8 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
     // two 88-VGPR pair waves the 168-VGPR kernel would fit two too -- measured the same on
     // cfg3, profiles/r03/ab_mac.txt)
     if (mac_many)
-        hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS, MAC_LB_MANY, MAC_PF_MANY>), grid, dim3(256), 0, s, recs, r1, pt,
-                           wire, states, wire_len, meta, tails, epoch, r0);
+        hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS, MAC_LB_MANY, MAC_PF_MANY>), grid, dim3(256), CFG_MAC_MANY_LDS, s,
+                           recs, r1, pt, wire, states, wire_len, meta, tails, epoch, r0);
     else
         hipLaunchKernelGGL((mac_kernel<MAC, SSL3, BS>), grid, dim3(256), 0, s, recs, r1, pt, wire, states, wire_len,
                            meta, tails, epoch, r0);

@@ -25,6 +25,9 @@
 #ifndef TG_AB_MAC_PF_MANY
 #define TG_AB_MAC_PF_MANY 1
 #endif
+#ifndef TG_AB_MAC_MANY_LDS
+#define TG_AB_MAC_MANY_LDS 0
+#endif
 #ifndef TG_AB_PAIR_WM
 #define TG_AB_PAIR_WM 8
 #endif
@@ -46,6 +49,7 @@ constexpr int CFG_MAC_PF = TG_AB_MAC_PF;
 constexpr int CFG_MAC_LB = TG_AB_MAC_LB;
 constexpr int CFG_MAC_LB_MANY = TG_AB_MAC_LB_MANY;
 constexpr int CFG_MAC_PF_MANY = TG_AB_MAC_PF_MANY;
+constexpr int CFG_MAC_MANY_LDS = TG_AB_MAC_MANY_LDS;
 constexpr int CFG_PAIR_WAVES_MANY = TG_AB_PAIR_WM;
 constexpr int CFG_PAIR_G1 = TG_AB_PAIR_G1;
 constexpr int CFG_PAIR_GM = TG_AB_PAIR_GM;
