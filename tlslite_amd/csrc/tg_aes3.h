@@ -662,7 +662,11 @@ struct PrioTurn {
         // unchanged at 20 + 5; the many-chains form (cfg3, 4-block groups) measured 552 -> 548
         // (profiles/r05/ab_seal.txt), so it keeps the fixed priority
         if constexpr (G >= 8) {
-            if (++turn & 1u) __builtin_amdgcn_s_setprio(BASE + 1);
+            // wave-uniform (an SGPR, so the branch is a scalar one): inside a chain's group loop
+            // the lanes of chains of different lengths would count differently, and a per-lane
+            // condition issues both s_setprio arms
+            turn = __builtin_amdgcn_readfirstlane(turn + 1u);
+            if (turn & 1u) __builtin_amdgcn_s_setprio(BASE + 1);
             else __builtin_amdgcn_s_setprio(BASE);
         }
     }
