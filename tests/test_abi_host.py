@@ -178,3 +178,33 @@ def test_oracle_fill_pattern_is_splitmix():
         return z ^ (z >> 31)
     exp = [(sm(7 + (g >> 3)) >> (8 * (g & 7))) & 0xff for g in range(3, 43)]
     assert a.tolist() == exp
+
+
+def test_no_kernel_gets_lds_it_does_not_declare():
+    """Static LDS of every kernel in the built gfx950 code object (AMDGPU metadata,
+    .group_segment_fixed_size) is only what the sources declare with __shared__: the frame
+    kernels' reduction scratch.  The AES / 3DES / RC4 kernels take their tables as dynamic LDS
+    at launch, and the MAC kernels must take none: the seal pipeline runs a MAC workgroup on a
+    CU beside the cipher kernel's 128 KiB of tables, and round 6 found the backend's
+    promote-alloca pass had given the MAC kernels 19 KiB each (build.py now disables it)."""
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    lib = os.path.join(ROOT, "tlslite_amd", "lib", "libtlsgpu.so")
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-objdump")):
+        pytest.skip("no llvm-objdump in this image")
+    with tempfile.TemporaryDirectory() as d:
+        shutil.copy(lib, d)
+        subprocess.check_call([os.path.join(llvm, "llvm-objdump"), "--offloading", "libtlsgpu.so"], cwd=d,
+                              stdout=subprocess.DEVNULL)
+        co = [f for f in os.listdir(d) if "gfx950" in f]
+        assert co, os.listdir(d)
+        notes = subprocess.check_output([os.path.join(llvm, "llvm-readelf"), "--notes", co[0]], cwd=d, text=True)
+    kernels = re.findall(r"\.group_segment_fixed_size:\s+(\d+).*?\.name:\s+(\S+)", notes, re.S)
+    assert len(kernels) >= 40
+    with_lds = {n for lds, n in kernels if int(lds) > 0}
+    allowed = ("frame_count_kernel", "frame_scan_kernel", "frame_write_kernel")
+    assert all(any(a in n for a in allowed) for n in with_lds), sorted(with_lds)
+    assert any("mac_kernel" in n for _, n in kernels)

@@ -47,8 +47,13 @@ def build(force=False, verbose=False, extra_flags=(), libdir=LIBDIR, overlay=Non
     incs = (["-I" + overlay] if overlay else []) + ["-I" + CSRC]
     if overlay:
         deps += [os.path.join(overlay, f) for f in os.listdir(overlay)]
+    # -disable-promote-alloca-to-lds: the AMDGPU backend may turn a kernel's private array into
+    # static LDS (round 6: the MAC kernels' funnel-shift words became 19 KiB per workgroup), which
+    # no source line shows and which takes the LDS the seal pipeline needs to run a MAC
+    # workgroup beside the cipher kernel's 128 KiB of tables (cfg3 -4.5 %, the concurrent open
+    # -18 %).  Kernels that want LDS declare it; tests/test_abi_host.py checks the code objects.
     flags = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-Wall", "-Wno-unused-function",
-             "-munsafe-fp-atomics"] + incs + list(extra_flags)
+             "-munsafe-fp-atomics", "-mllvm", "-disable-promote-alloca-to-lds"] + incs + list(extra_flags)
     if not force and not _stale(lib, deps):
         return lib
     for s in srcs:

@@ -15,7 +15,7 @@ for i in $(seq 1 $N); do
     timeout -k 10 300 python bench.py --config $CFG --no-host-inclusive --no-open --no-derive --no-cpu --no-check $AB_ARGS \
         > $O/${CFG}_${v}_$i.json 2> $O/${CFG}_${v}_$i.err || { tail -20 $O/${CFG}_${v}_$i.err; exit 1; }
     python -c "
-import json;d=json.load(open('$O/${CFG}_${v}_$i.json'));print('$CFG $v', d['value'], d['ms_per_step'], d['roofline']['kernel_avg_ms'], d['ms_per_seal_call'])"
+import json;d=json.load(open('$O/${CFG}_${v}_$i.json'));o=d.get('open') or {};print('$CFG $v', d['value'], d['ms_per_step'], d['roofline']['kernel_avg_ms'], d['ms_per_seal_call'], 'open', o.get('value'), (o.get('concurrent') or {}).get('value'))"
   done
 done
 unset TLSGPU_LIB
