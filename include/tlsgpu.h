@@ -403,7 +403,7 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t *rx_host, si
  * announcing an empty body: the reference raises TLSAbruptCloseError there, so the records
  * before it are framed and the connection stops), TLSGPU_EINVAL (the span
  * leaves the arena).  Records past max_records are not framed (consumed[] stops before
- * them).  total (device, one uint32) = records framed.  The result feeds tlsgpu_open_dev
+ * them).  total (device, one uint32) = records framed (0 for n = 0).  The result feeds tlsgpu_open_dev
  * directly (nrecords = max_records, or *total read back), with a plaintext arena of
  * stream_bytes.  Everything is device memory; workspace: tlsgpu_frame_workspace_bytes(n),
  * 8-byte aligned. */

@@ -1209,7 +1209,10 @@ int tlsgpu_frame_dev(const uint8_t* stream, size_t stream_bytes, const tlsgpu_sp
                      tlsgpu_open_record* records, uint32_t max_records, tlsgpu_chain* chains, uint32_t chain_flags,
                      uint32_t* consumed, int32_t* status, uint32_t* total, void* workspace, size_t workspace_bytes,
                      tlsgpu_stream s) {
-    if (n == 0) return 0;
+    if (n == 0) {  // nothing framed: total = 0 (stream-ordered, as the kernels would write it)
+        if (total) TG_HIP(hipMemsetAsync(total, 0, 4, HS(s)));
+        return 0;
+    }
     if (!stream || !conns || !chains || !consumed || !status || !total || !workspace || (!records && max_records))
         return fail(TLSGPU_EINVAL, "null pointer");
     if (n > (1u << 26)) return fail(TLSGPU_EINVAL, "too many connections");
