@@ -66,7 +66,8 @@ def test_zero_sized_calls():
         b.free()
 
 
-@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES256-SHA256", (3, 1)), ("3DES-SHA", (3, 2)),
+@pytest.mark.parametrize("suite,version", [("AES128-SHA", (3, 3)), ("AES256-SHA256", (3, 3)), ("AES256-SHA", (3, 1)),
+                                           ("3DES-SHA", (3, 2)),
                                            ("RC4-SHA", (3, 1)), ("RC4-MD5", (3, 0))])
 def test_chains_without_records(suite, version):
     from oracle import oracle as O
