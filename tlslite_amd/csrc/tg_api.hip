@@ -846,6 +846,9 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
             stage_copy(p->pt_stage[t].u8(), src, b.p1 - b.p0);
             src = p->pt_stage[t].u8();
         }
+        // (CFG_HOST_H2D_LEAD) sub-batch i - L's seal_done is slot (i - L) % D's latest record for L <= D
+        const size_t lead = CFG_HOST_H2D_LEAD < 1 ? 0 : CFG_HOST_H2D_LEAD > D ? (size_t)D : (size_t)CFG_HOST_H2D_LEAD;
+        if (pt_direct && lead && i >= lead) TG_HIP(hipStreamWaitEvent(p->h2d, p->seal_done[(i - lead) % D], 0));
         if (b.p1 > b.p0) TG_HIP(hipMemcpyAsync(p->pt.u8() + b.p0, src, b.p1 - b.p0, hipMemcpyHostToDevice, p->h2d));
         TG_HIP(hipEventRecord(p->in_done[t], p->h2d));
         TG_HIP(hipStreamWaitEvent(p->mac, p->in_done[t], 0));

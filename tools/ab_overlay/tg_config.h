@@ -41,6 +41,9 @@
 #define TG_AB_PIPE_WS 3
 #endif
 
+#ifndef TG_AB_H2D_LEAD
+#define TG_AB_H2D_LEAD 0
+#endif
 namespace tg {
 constexpr int CFG_CBC_WAVES = TG_AB_CBC_WAVES;
 constexpr int CFG_MAC_PRIO = TG_AB_MAC_PRIO;
@@ -54,4 +57,5 @@ constexpr int CFG_PAIR_WAVES_MANY = TG_AB_PAIR_WM;
 constexpr int CFG_PAIR_G1 = TG_AB_PAIR_G1;
 constexpr int CFG_PAIR_GM = TG_AB_PAIR_GM;
 constexpr int CFG_PIPE_WS = TG_AB_PIPE_WS;
+constexpr int CFG_HOST_H2D_LEAD = TG_AB_H2D_LEAD;
 }  // namespace tg
