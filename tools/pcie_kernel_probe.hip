@@ -9,6 +9,17 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+// NUMA node of the page holding p (move_pages with no target nodes only reports), -1 if unknown
+static int numa_node_of(void* p) {
+    void* pages[1] = {p};
+    int status[1] = {-1};
+    if (syscall(SYS_move_pages, 0, 1, pages, nullptr, status, 0) != 0) return -1;
+    return status[0];
+}
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
@@ -40,13 +51,16 @@ __global__ void __launch_bounds__(256) copy_kernel(const u32x4* __restrict__ src
     for (; i < n16; i += stride) dst[i] = src[i];
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool quick = argc > 1 && !strcmp(argv[1], "quick");
     const size_t N = (size_t)1 << 30;
     void *h_in, *h_out, *d_in, *d_out, *hd_in, *hd_out;
     CK(hipHostMalloc(&h_in, N, hipHostMallocDefault));
     CK(hipHostMalloc(&h_out, N, hipHostMallocDefault));
     memset(h_in, 1, N);
     memset(h_out, 2, N);
+    printf("process on cpu %d; h_in on NUMA node %d, h_out on node %d\n", sched_getcpu(), numa_node_of(h_in),
+           numa_node_of(h_out));
     CK(hipHostGetDevicePointer(&hd_in, h_in, 0));
     CK(hipHostGetDevicePointer(&hd_out, h_out, 0));
     CK(hipMalloc(&d_in, N));
@@ -77,8 +91,12 @@ int main() {
         {"H2D kernel g256 + D2H kernel g256", 3, true, true, false, 256},
     };
     for (size_t piece : {N, (size_t)64 << 20}) {
+    if (quick && piece == N) continue;
     printf("-- copies of %zu MiB\n", piece >> 20);
     for (const Mode& m : modes) {
+        if (quick && strcmp(m.name, "D2H sdma") && strcmp(m.name, "both sdma") && strcmp(m.name, "D2H kernel g256") &&
+            strcmp(m.name, "H2D sdma + D2H kernel g256"))
+            continue;
         double best = 1e9, bh = 1e9, bd = 1e9;
         for (int rep = 0; rep < 4; rep++) {
             CK(hipDeviceSynchronize());
