@@ -300,7 +300,8 @@ def pcie_rates(nbytes=256 << 20):
     """Measured pinned copy rates on this box with the HIP runtime directly (ctypes on
     libamdhip64, the engines the host pipeline uses): H2D alone, D2H alone, and both
     at once on two streams (GB/s; the last is the total of both directions).  Same
-    method as tools/pcie_probe.hip."""
+    method as tools/pcie_probe.hip.  Plus the host pipelines' other D2H path, the GPU's own
+    stores (tlsgpu_host_store): alone (d2h_stores) and beside an H2D copy (both_stores)."""
     import ctypes
     hip = ctypes.CDLL("libamdhip64.so")
     vp = ctypes.c_void_p
@@ -315,21 +316,25 @@ def pcie_rates(nbytes=256 << 20):
     hip.hipStreamCreateWithFlags(ctypes.byref(s2), 1)
     hip.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
     res = {}
-    for name, mode in (("warm", 3), ("h2d", 1), ("d2h", 2), ("both", 3)):  # "warm": untimed first copies
-        best = None
+    from tlslite_amd import _native as N
+    for name, mode in (("warm", 3), ("h2d", 1), ("d2h", 2), ("both", 3), ("d2h_stores", 6), ("both_stores", 7)):
+        best = None  # "warm": untimed first copies; mode bit 2: the D2H copy by device stores
         for _ in range(6 if name != "warm" else 2):
             hip.hipDeviceSynchronize()
             t0 = time.perf_counter()
             if mode & 1:
                 hip.hipMemcpyAsync(d1, h1, nbytes, 1, s1)
             if mode & 2:
-                hip.hipMemcpyAsync(h2, d2, nbytes, 2, s2)
+                if mode & 4:
+                    N.call("tlsgpu_host_store", h2, d2, nbytes, s2)
+                else:
+                    hip.hipMemcpyAsync(h2, d2, nbytes, 2, s2)
             hip.hipStreamSynchronize(s1)
             hip.hipStreamSynchronize(s2)
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
         if name != "warm":
-            res[name] = round(nbytes * (2 if mode == 3 else 1) / best / 1e9, 1)
+            res[name] = round(nbytes * (2 if mode & 1 and mode & 2 else 1) / best / 1e9, 1)
     for ptr in (h1, h2):
         hip.hipHostFree(ptr)
     for ptr in (d1, d2):
@@ -337,6 +342,11 @@ def pcie_rates(nbytes=256 << 20):
     hip.hipStreamDestroy(s1)
     hip.hipStreamDestroy(s2)
     return res
+
+
+def link_best(link):
+    """(D2H GB/s, both-directions GB/s) of the better D2H path in pcie_rates' measurements."""
+    return (max(link["d2h"], link.get("d2h_stores") or 0.0), max(link["both"], link.get("both_stores") or 0.0))
 
 
 def host_inclusive_rate(wl, chunk=64 << 20, depth=3):
@@ -366,10 +376,12 @@ def host_inclusive_rate(wl, chunk=64 << 20, depth=3):
     link = pcie_rates()
     if link:
         # both directions at once share the link: the copies need at least
-        # max(H2D bytes / H2D rate, D2H bytes / D2H rate, all bytes / both-at-once rate)
-        t_min = max(wl.pt_bytes / (link["h2d"] * 1e9), wl.wire_bytes / (link["d2h"] * 1e9),
-                    (wl.pt_bytes + wl.wire_bytes) / (link["both"] * 1e9))
-        how = "measured pinned hipMemcpyAsync rates on this box (pcie_measured_gbs)"
+        # max(H2D bytes / H2D rate, D2H bytes / D2H rate, all bytes / both-at-once rate),
+        # the D2H rates the better of the pipeline's two D2H paths
+        d2h, both = link_best(link)
+        t_min = max(wl.pt_bytes / (link["h2d"] * 1e9), wl.wire_bytes / (d2h * 1e9),
+                    (wl.pt_bytes + wl.wire_bytes) / (both * 1e9))
+        how = "measured pinned copy rates on this box (pcie_measured_gbs; D2H: copy engine or device stores)"
     else:
         t_min = max(wl.pt_bytes, wl.wire_bytes) / (PCIE_GBS * 1e9)
         how = "63 GB/s per direction, full duplex (spec)"
@@ -396,6 +408,7 @@ def host_inclusive_rate(wl, chunk=64 << 20, depth=3):
             exact = bool(np.array_equal(wire_h, ref)) and bool(np.array_equal(lens, wl.wire_len.astype(np.int32)))
             out[name] = {"value": round(wl.plaintext_total / GIB / best, 2), "ms": round(best * 1e3, 3),
                          "bit_exact": exact}
+        out["d2h_path"] = hp.d2h_path
     out["value"] = out["pinned"]["value"]
     out["pcie_frac"] = round(out["value"] / out["pcie_ceiling"], 3)
     pin_pt.free()
@@ -452,8 +465,9 @@ def host_open_rate(wl, link=None, chunk=64 << 20, depth=3):
     sp[:, 12:16] = np.arange(wl.n_chains, dtype=np.uint32).reshape(-1, 1).view(np.uint8)
     link = link or pcie_rates()
     if link:
-        t_min = max(nbytes / (link["h2d"] * 1e9), nbytes / (link["d2h"] * 1e9), 2 * nbytes / (link["both"] * 1e9))
-        how = "measured pinned hipMemcpyAsync rates on this box (pcie_measured_gbs)"
+        d2h, both = link_best(link)
+        t_min = max(nbytes / (link["h2d"] * 1e9), nbytes / (d2h * 1e9), 2 * nbytes / (both * 1e9))
+        how = "measured pinned copy rates on this box (pcie_measured_gbs; D2H: copy engine or device stores)"
     else:
         t_min = nbytes / (PCIE_GBS * 1e9)
         how = "63 GB/s per direction, full duplex (spec)"
@@ -492,6 +506,7 @@ def host_open_rate(wl, link=None, chunk=64 << 20, depth=3):
                         break
             out[name] = {"value": round(wl.plaintext_total / GIB / best, 2), "ms": round(best * 1e3, 3),
                          "roundtrip_exact": exact}
+        out["d2h_path"] = hp.d2h_path
     out["value"] = out["pinned"]["value"]
     out["pcie_frac"] = round(out["value"] / out["pcie_ceiling"], 3)
     pin_rx.free()

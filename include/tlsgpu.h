@@ -329,6 +329,16 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain *chains
                               const tlsgpu_record *records, uint32_t nrecords, const uint8_t *pt_host,
                               size_t pt_bytes, uint8_t *wire_host, size_t wire_bytes, tlsgpu_conn_state *states,
                               uint32_t nstates, int32_t *wire_len_host, uint32_t variant);
+/* The host pipelines' large D2H copies (wire ranges, opened plaintext) go by the copy engine or
+ * by the GPU's own stores into the pinned destination (tlsgpu_host_store's kernel): each pipeline
+ * times both on its first call (32 MiB, ~3 ms) and keeps the stores only when they are >= 1.25x
+ * faster -- in some processes the engine's D2H runs at about half its usual rate while the
+ * stores do not.  TLSGPU_HOST_D2H=engine|kernel in the environment
+ * forces a path.  *path: -1 not chosen yet, 0 copy engine, 1 device stores. */
+int tlsgpu_host_pipeline_d2h_path(tlsgpu_host_pipeline p, int *path);
+/* D2H copy by device stores, async on s: dst_host is pinned host memory (tlsgpu_host_alloc) at
+ * the same address mod 16 as src_dev; TLSGPU_EINVAL otherwise. */
+int tlsgpu_host_store(void *dst_host, const void *src_dev, size_t bytes, tlsgpu_stream s);
 
 /* Batch open: status[r] = plaintext length, or TLSGPU_ALERT_* (records 0..nrecords-1;
  * a chain's records open in order on its state, as successive _decryptRecord calls).

@@ -117,7 +117,8 @@ def _expect(O, streams, oreaders, max_records):
     ("RC4-SHA", (3, 1), True, 3, 24 << 10, None),
     ("RC4-MD5", (3, 0), False, 3, 64 << 10, 0.3),
 ])
-def test_host_pipeline_open_vs_oracle(suite, version, pinned, depth, chunk, cut):
+@pytest.mark.parametrize("d2h", ["engine", "stores"])
+def test_host_pipeline_open_vs_oracle(suite, version, pinned, depth, chunk, cut, d2h, monkeypatch):
     from oracle import oracle as O
     T = _T()
     from tlslite_amd import _native as N
@@ -136,8 +137,10 @@ def test_host_pipeline_open_vs_oracle(suite, version, pinned, depth, chunk, cut)
     d_states = DeviceBuffer(pack_states(readers).size)
     d_states.upload(pack_states(readers))
     want = _expect(O, streams, oreaders, maxr)
+    monkeypatch.setenv("TLSGPU_HOST_D2H", "kernel" if d2h == "stores" else "engine")
     with HostSealPipeline(chunk, depth) as hp:
         res = hp.open(rx, spans, pt, d_states, readers[0].variant, max_records=maxr)
+        assert hp.d2h_path == d2h
     assert res["total"] == sum(len(w[2]) for w in want) <= maxr
     recs = np.frombuffer(res["records"], dtype=np.uint8).reshape(-1, 24)
     ch = np.frombuffer(res["chains"], dtype=np.uint32).reshape(nconn, 4)
@@ -170,3 +173,34 @@ def test_host_pipeline_open_vs_oracle(suite, version, pinned, depth, chunk, cut)
         assert (r.rc4 == o.rc4) if O.SUITES[suite][0] == "rc4" else (r.iv == o.iv)
     for b in keep:
         b.free()
+
+
+def test_host_store_copies_exactly():
+    """tlsgpu_host_store (a D2H copy by the GPU's own stores, the host pipelines' other D2H path):
+    every byte of ranges with ragged heads and tails lands, nothing around them is written, a
+    destination that is not pinned or differs mod 16 is refused; and a fresh pipeline's first
+    call chooses a path (calibration) without changing its results."""
+    _T()
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import DeviceBuffer, PinnedBuffer, Stream
+    rng = np.random.default_rng(7)
+    n = (3 << 20) + 77
+    src = rng.integers(0, 256, n, dtype=np.uint8)
+    d = DeviceBuffer(n)
+    d.upload(src)
+    h = PinnedBuffer(n)
+    s = Stream()
+    for off, ln in [(0, n), (1, 15), (5, 16), (11, 4096 + 3), (16, 1 << 20), (7, 0), (13, 2), (3, (2 << 20) + 1)]:
+        h.array[:n] = 0xEE
+        N.call("tlsgpu_host_store", h.ptr.value + off, d.addr + off, ln, s.handle)
+        s.synchronize()
+        got = h.array[:n]
+        assert np.array_equal(got[off:off + ln], src[off:off + ln]), (off, ln)
+        assert (got[:off] == 0xEE).all() and (got[off + ln:] == 0xEE).all(), (off, ln)
+    with pytest.raises(N.TLSGPUError):
+        N.call("tlsgpu_host_store", h.ptr.value + 1, d.addr, 64, s.handle)  # differ mod 16
+    pageable = np.zeros(64, dtype=np.uint8)
+    with pytest.raises(N.TLSGPUError):
+        N.call("tlsgpu_host_store", pageable.ctypes.data, d.addr, 64, s.handle)
+    d.free()
+    h.free()

@@ -313,13 +313,16 @@ def test_unaligned_arenas_pair_regime(pt_shift, wire_shift, suite, version):
 
 @pytest.mark.parametrize("kind", ["cfg2", "chained", "shuffled", "rc4", "3des"])
 @pytest.mark.parametrize("pinned", [True, False])
-def test_host_pipeline_equals_device_path(kind, pinned):
+@pytest.mark.parametrize("d2h", ["engine", "stores"])
+def test_host_pipeline_equals_device_path(kind, pinned, d2h, monkeypatch):
     """tlsgpu_host_pipeline_seal (records in host memory; sub-batches' H2D, seal and
     D2H overlapped on 3 streams, pageable buffers staged through pinned ones) gives
     the same wire arena, wire lengths and final states as the device-resident
     tlsgpu_seal_dev path -- with a small chunk so the batch is cut into many
     sub-batches, for a shuffled arena layout (one sub-batch), and for the RC4
-    single-kernel branch and the 3DES split path (TLS 1.0 and 1.2 records)."""
+    single-kernel branch and the 3DES split path (TLS 1.0 and 1.2 records); with the wire
+    ranges copied D2H by the copy engine and by the GPU's own stores (TLSGPU_HOST_D2H)."""
+    monkeypatch.setenv("TLSGPU_HOST_D2H", "kernel" if d2h == "stores" else "engine")
     _T()
     from tlslite_amd import workloads as W
     from tlslite_amd.constants import ContentType
@@ -355,6 +358,7 @@ def test_host_pipeline_equals_device_path(kind, pinned):
     synchronize()
     with HostSealPipeline(chunk_bytes=64 << 10, depth=3) as hp:
         hp.seal(chains, recs, pt_h, wire_h, wl.d_states, lens, var)
+        assert hp.d2h_path == d2h
     assert lens.tolist() == wl.wire_len.astype(np.int32).tolist()
     bad = np.nonzero(wire_h != ref_wire)[0]
     bad_recs = sorted(set(int(np.searchsorted(wl.wire_off.astype(np.int64), x, side="right")) - 1 for x in bad[:4096]))

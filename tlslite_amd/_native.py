@@ -108,6 +108,8 @@ SIGNATURES = [
     ("tlsgpu_host_pipeline_create", _i, [ctypes.POINTER(_vp), _sz, _i]),
     ("tlsgpu_host_pipeline_destroy", _i, [_vp]),
     ("tlsgpu_host_pipeline_seal", _i, [_vp, _vp, _u32, _vp, _u32, _vp, _sz, _vp, _sz, _vp, _u32, _vp, _u32]),
+    ("tlsgpu_host_pipeline_d2h_path", _i, [_vp, _vp]),
+    ("tlsgpu_host_store", _i, [_vp, _vp, _sz, _vp]),
     ("tlsgpu_host_pipeline_open", _i, [_vp, _vp, _sz, _vp, _u32, _u32, _vp, _sz, _vp, _u32, _u32, _vp, _u32, _vp, _vp,
                                        _vp, _vp, _vp]),
     ("tlsgpu_open_workspace_bytes", _sz, [_u32]),

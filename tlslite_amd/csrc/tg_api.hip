@@ -561,6 +561,19 @@ bool host_pinned(const void* ptr) {
     }
     return a.type == hipMemoryTypeHost;
 }
+// Pinned host memory the GPU can store into at its own address (ROCm maps pinned host memory at
+// the same virtual address on the device): that address, or nullptr (the copy engine only)
+uint8_t* host_store_ptr(void* h) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, h) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.hostPointer || !a.devicePointer) return nullptr;
+    // h's device address, whether the runtime reports the allocation's base or h itself
+    uint8_t* d = static_cast<uint8_t*>(a.devicePointer) + (static_cast<uint8_t*>(h) - static_cast<uint8_t*>(a.hostPointer));
+    return d == h ? d : nullptr;
+}
 // Staging copies between pageable host memory and the pinned buffers: one thread moves
 // ~10 GB/s, below the link's 57 GB/s per direction, so large copies are split over a few
 // threads (at most 8: the job's share of host cores on the GPU box is 16).
@@ -623,7 +636,84 @@ struct tlsgpu_host_pipeline_s {
     PinBuf h_totals;
     std::vector<hipEvent_t> framed, opened;
     std::vector<hipEvent_t> rx_in;  // per sub-batch of a receive call: its H2D copy is done
+    int d2h_path = -1;              // D2H by: -1 not chosen yet, 0 the copy engine, 1 the GPU's stores
 };
+
+// The host pipelines' big D2H copies (wire / plaintext ranges) go by the copy engine or by the
+// GPU's own stores (host_store_kernel).  On most boxes the engine is the faster one beside the
+// H2D copies (56 + 48 GB/s against 43 + 50), but in about one process in four its D2H runs at
+// 30 GB/s where the stores still reach 55 (profiles/r06/hostpipe/NOTES.md).  So each pipeline
+// times both once, on its first call (32 MiB each, best of 3, ~3 ms), and takes the stores only
+// when they are >= 1.25x faster.  TLSGPU_HOST_D2H=engine|kernel forces a path (tests).
+static int choose_d2h_path(tlsgpu_host_pipeline p) {
+    if (p->d2h_path >= 0) return 0;
+    const char* env = getenv("TLSGPU_HOST_D2H");
+    if (env && !strcmp(env, "engine")) {
+        p->d2h_path = 0;
+        return 0;
+    }
+    if (env && !strcmp(env, "kernel")) {
+        p->d2h_path = 1;
+        return 0;
+    }
+    const size_t n = (size_t)32 << 20;
+    DevBuf src;
+    PinBuf dst;
+    TG_HIP(src.ensure(n));
+    TG_HIP(dst.ensure(n));
+    uint8_t* dd = host_store_ptr(dst.p);
+    float best[2] = {1e30f, 1e30f};
+    if (dd) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        TG_HIP(hipEventCreate(&e0));
+        TG_HIP(hipEventCreate(&e1));
+        hipError_t e = hipMemsetAsync(src.p, 0, n, p->d2h);
+        for (int rep = 0; rep < 4 && e == hipSuccess; rep++)
+            for (int k = 0; k < 2 && e == hipSuccess; k++) {
+                e = hipEventRecord(e0, p->d2h);
+                if (e == hipSuccess)
+                    e = k ? launch_host_store(src.u8(), dd, n, p->d2h)
+                          : hipMemcpyAsync(dst.p, src.p, n, hipMemcpyDeviceToHost, p->d2h);
+                if (e == hipSuccess) e = hipEventRecord(e1, p->d2h);
+                if (e == hipSuccess) e = hipEventSynchronize(e1);
+                float ms = 0;
+                if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+                if (e == hipSuccess && rep) best[k] = ms < best[k] ? ms : best[k];
+            }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (e != hipSuccess) return fail_hip(e, "host pipeline D2H calibration");
+    }
+    src.release();
+    dst.release();
+    p->d2h_path = best[1] * 1.25f < best[0] ? 1 : 0;
+    return 0;
+}
+
+// one big D2H range of a host pipeline: dst is pinned host memory (the caller's or a stage) at
+// the same address mod 16 as src; by the GPU's stores where chosen and possible
+static hipError_t pipeline_d2h(tlsgpu_host_pipeline p, uint8_t* dst, uint8_t* dst_dev, const uint8_t* src, size_t n) {
+    if (p->d2h_path == 1 && dst_dev && !(((uintptr_t)src ^ (uintptr_t)dst_dev) & 15))
+        return launch_host_store(src, dst_dev, n, p->d2h);
+    return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, p->d2h);
+}
+
+int tlsgpu_host_pipeline_d2h_path(tlsgpu_host_pipeline p, int* path) {
+    if (!p || !path) return fail(TLSGPU_EINVAL, "null");
+    *path = p->d2h_path;
+    return 0;
+}
+
+int tlsgpu_host_store(void* dst_host, const void* src_dev, size_t bytes, tlsgpu_stream s) {
+    if (!bytes) return 0;
+    if (!dst_host || !src_dev) return fail(TLSGPU_EINVAL, "null pointer");
+    uint8_t* dd = host_store_ptr(dst_host);
+    if (!dd) return fail(TLSGPU_EINVAL, "destination is not pinned host memory the device can store into");
+    if (((uintptr_t)dd ^ (uintptr_t)src_dev) & 15) return fail(TLSGPU_EINVAL, "source and destination differ mod 16");
+    hipError_t e = launch_host_store(static_cast<const uint8_t*>(src_dev), dd, bytes, HS(s));
+    if (e != hipSuccess) return fail_hip(e, "host store launch");
+    return 0;
+}
 
 int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, int depth) {
     if (!out) return fail(TLSGPU_EINVAL, "null");
@@ -802,6 +892,11 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
     }
     const int D = p->depth;
     const bool pt_direct = host_pinned(pt_host), wire_direct = host_pinned(wire_host);
+    {
+        int rc = choose_d2h_path(p);
+        if (rc) return rc;
+    }
+    uint8_t* wire_dev = wire_direct ? host_store_ptr(wire_host) : nullptr;
     size_t max_p = 0, max_w = 0;
     for (const SubBatch& b : sub) {
         max_p = b.p1 - b.p0 > max_p ? b.p1 - b.p0 : max_p;
@@ -818,7 +913,7 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
     for (int i = 0; i < D; i++) {
         if (need_ws) TG_HIP(p->ws[i].ensure(seal_workspace_bytes(nrecords)));
         if (!pt_direct) TG_HIP(p->pt_stage[i].ensure(max_p));
-        if (!wire_direct) TG_HIP(p->wire_stage[i].ensure(max_w));
+        if (!wire_direct) TG_HIP(p->wire_stage[i].ensure(max_w + 16));  // + the range's offset mod 16
     }
     // descriptors once (small), on the h2d stream ahead of the first sub-batch's plaintext
     TG_HIP(hipMemcpyAsync(p->recs.p, records, (size_t)nrecords * sizeof(tlsgpu_record), hipMemcpyHostToDevice, p->h2d));
@@ -829,7 +924,8 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
     auto drain = [&](size_t j) -> int {
         const int t = (int)(j % D);
         TG_HIP(hipEventSynchronize(p->out_done[t]));
-        if (!wire_direct) stage_copy(wire_host + sub[j].w0, p->wire_stage[t].u8(), sub[j].w1 - sub[j].w0);
+        if (!wire_direct)
+            stage_copy(wire_host + sub[j].w0, p->wire_stage[t].u8() + (sub[j].w0 & 15), sub[j].w1 - sub[j].w0);
         return 0;
     };
     // Pinned arenas: everything is enqueued at once and ordered on the GPU (slot t's seal
@@ -883,8 +979,11 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
             if (rc) return rc;
         }
         TG_HIP(hipStreamWaitEvent(p->d2h, p->seal_done[t], 0));
-        uint8_t* dst = wire_direct ? wire_host + b.w0 : p->wire_stage[t].u8();
-        if (b.w1 > b.w0) TG_HIP(hipMemcpyAsync(dst, p->wire.u8() + b.w0, b.w1 - b.w0, hipMemcpyDeviceToHost, p->d2h));
+        // the stage holds the range at the same offset mod 16 as the device arena (stores path)
+        uint8_t* dst = wire_direct ? wire_host + b.w0 : p->wire_stage[t].u8() + (b.w0 & 15);
+        uint8_t* dst_dev = wire_direct ? (wire_dev ? wire_dev + b.w0 : nullptr) : host_store_ptr(p->wire_stage[t].p);
+        if (dst_dev && !wire_direct) dst_dev += b.w0 & 15;
+        if (b.w1 > b.w0) TG_HIP(pipeline_d2h(p, dst, dst_dev, p->wire.u8() + b.w0, b.w1 - b.w0));
         TG_HIP(hipEventRecord(p->out_done[t], p->d2h));
     }
     if (wire_direct) {
@@ -985,6 +1084,11 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
     const int D = p->depth;
     const size_t nsub = sub.size();
     const bool rx_direct = host_pinned(rx_host), pt_direct = host_pinned(pt_host);
+    {
+        int rc = choose_d2h_path(p);
+        if (rc) return rc;
+    }
+    uint8_t* pt_dev = pt_direct ? host_store_ptr(pt_host) : nullptr;
     const bool out_direct = max_records == 0 || (host_pinned(records_host) && host_pinned(status_host));
     const bool need_ws = open_needs_workspace(variant);
     uint64_t cap_max = 1, span_max = 0;
@@ -1014,7 +1118,7 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
         if (need_ws) TG_HIP(p->rws[t].ensure(open_workspace_bytes((uint32_t)cap_max)));
         TG_HIP(p->fws[t].ensure(frame_workspace_bytes(nc_max)));
         if (!rx_direct) TG_HIP(p->rx_stage[t].ensure(span_max));
-        if (!pt_direct) TG_HIP(p->opt_stage[t].ensure(span_max));
+        if (!pt_direct) TG_HIP(p->opt_stage[t].ensure(span_max + 16));  // + the range's offset mod 16
     }
     // the D2H ranges come back zero outside the opened bodies, never bytes of an earlier call
     TG_HIP(hipMemsetAsync(p->opt.p, 0, rx_bytes, p->h2d));
@@ -1088,8 +1192,10 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
         TG_HIP(hipEventRecord(p->opened[t], ks));
         TG_HIP(hipStreamWaitEvent(p->d2h, p->opened[t], 0));
         if (b.b1 > b.b0) {
-            uint8_t* dst = pt_direct ? pt_host + b.b0 : p->opt_stage[t].u8();
-            TG_HIP(hipMemcpyAsync(dst, p->opt.u8() + b.b0, b.b1 - b.b0, hipMemcpyDeviceToHost, p->d2h));
+            uint8_t* dst = pt_direct ? pt_host + b.b0 : p->opt_stage[t].u8() + (b.b0 & 15);
+            uint8_t* dst_dev = pt_direct ? (pt_dev ? pt_dev + b.b0 : nullptr) : host_store_ptr(p->opt_stage[t].p);
+            if (dst_dev && !pt_direct) dst_dev += b.b0 & 15;
+            TG_HIP(pipeline_d2h(p, dst, dst_dev, p->opt.u8() + b.b0, b.b1 - b.b0));
         }
         if (T) {
             void* rd = records_host + base[i];
@@ -1112,7 +1218,7 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
         const int t = (int)(j % D);
         TG_HIP(hipEventSynchronize(p->out_done[t]));
         if (!pt_direct && sub[j].b1 > sub[j].b0)
-            stage_copy(pt_host + sub[j].b0, p->opt_stage[t].u8(), sub[j].b1 - sub[j].b0);
+            stage_copy(pt_host + sub[j].b0, p->opt_stage[t].u8() + (sub[j].b0 & 15), sub[j].b1 - sub[j].b0);
         if (!out_direct && tot[j]) {
             memcpy(records_host + base[j], p->recs_stage[t].p, (size_t)tot[j] * sizeof(tlsgpu_open_record));
             memcpy(status_host + base[j], p->stat_stage[t].p, (size_t)tot[j] * 4);

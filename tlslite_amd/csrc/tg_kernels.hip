@@ -7,6 +7,7 @@
 //                    surface (python_aes.py:20-69, python_rc4.py:25-41)
 //   derive_kernel    batched _calcPendingStates (tg_derive.h)
 //   fill_kernel      deterministic synthetic input (splitmix64 byte stream)
+//   host_store_kernel  D2H copy by the GPU's own stores into pinned host memory (host pipelines)
 // The library has exactly one kernel per (direction, suite variant): no runtime
 // selection between implementations.
 #include <atomic>
@@ -379,6 +380,40 @@ __global__ void fill_kernel(uint8_t* __restrict__ p, size_t bytes, uint64_t seed
     } else {
         for (size_t b = 0; i0 + b < bytes; b++) p[i0 + b] = (uint8_t)(d[b >> 2] >> (8 * (b & 3)));
     }
+}
+
+// A device-to-host copy done by the GPU's own stores into pinned, device-mapped host memory
+// (tlsgpu_host_pipeline_*: where the copy engine's D2H runs slow).  src and dst
+// have the same address mod 16: byte copies up to the first 16-B boundary and after the last,
+// the body in 16-B words, four loads in flight per lane (grid-stride).  Vector stores only.
+__global__ void __launch_bounds__(256) host_store_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                         size_t n) {
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x, nth = (size_t)gridDim.x * blockDim.x;
+    size_t head = (16 - ((uintptr_t)src & 15)) & 15;
+    head = head < n ? head : n;
+    const size_t body = (n - head) >> 4, tail0 = head + (body << 4);
+    if (tid < head) dst[tid] = src[tid];
+    if (tid < n - tail0) dst[tail0 + tid] = src[tail0 + tid];
+    const uint4* __restrict__ s = reinterpret_cast<const uint4*>(src + head);
+    uint4* __restrict__ d = reinterpret_cast<uint4*>(dst + head);
+    size_t i = tid;
+    for (; i + 3 * nth < body; i += 4 * nth) {
+        const uint4 a = s[i], b = s[i + nth], c = s[i + 2 * nth], e = s[i + 3 * nth];
+        d[i] = a;
+        d[i + nth] = b;
+        d[i + 2 * nth] = c;
+        d[i + 3 * nth] = e;
+    }
+    for (; i < body; i += nth) d[i] = s[i];
+}
+
+hipError_t launch_host_store(const uint8_t* src, uint8_t* dst_dev, size_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    if (((uintptr_t)src ^ (uintptr_t)dst_dev) & 15) return hipErrorInvalidValue;
+    // 128 workgroups: the probe's rate (55 GB/s) from 64 up, and few enough to sit beside the
+    // seal / open kernels without taking their CUs (no LDS)
+    hipLaunchKernelGGL(host_store_kernel, dim3(128), dim3(256), 0, s, src, dst_dev, n);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- seal launchers

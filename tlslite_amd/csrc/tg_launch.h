@@ -70,5 +70,8 @@ int set_open_parts(int mode, long long min_records);
 hipError_t launch_derive(const tlsgpu_derive_desc* descs, uint32_t n, ConnState* ws, ConnState* rs,
                          uint8_t* master_out, uint8_t* kb_out, int32_t* status, hipStream_t s);
 hipError_t launch_fill(uint8_t* p, size_t bytes, uint64_t seed, uint64_t start, hipStream_t s);
+// D2H copy by device stores: dst_dev = the device address of pinned host memory, same address
+// mod 16 as src (hipErrorInvalidValue otherwise)
+hipError_t launch_host_store(const uint8_t* src, uint8_t* dst_dev, size_t n, hipStream_t s);
 
 }  // namespace tg

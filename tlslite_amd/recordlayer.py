@@ -263,6 +263,14 @@ class HostSealPipeline:
         return {"records": recs, "status": status[: total.value], "chains": chains, "consumed": consumed,
                 "frame_status": fstatus, "total": total.value}
 
+    @property
+    def d2h_path(self):
+        """How the pipeline's large D2H copies run: None (not chosen yet), "engine" (the copy
+        engine) or "stores" (the GPU's own stores into the pinned destination)."""
+        v = ctypes.c_int()
+        N.call("tlsgpu_host_pipeline_d2h_path", self.handle, ctypes.byref(v))
+        return {-1: None, 0: "engine", 1: "stores"}[v.value]
+
     def close(self):
         if self.handle is not None and self.handle.value:
             N.call("tlsgpu_host_pipeline_destroy", self.handle)
