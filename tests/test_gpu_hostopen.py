@@ -204,3 +204,40 @@ def test_host_store_copies_exactly():
         N.call("tlsgpu_host_store", pageable.ctypes.data, d.addr, 64, s.handle)
     d.free()
     h.free()
+
+
+def test_host_pipeline_chooses_d2h_path(monkeypatch):
+    """Without TLSGPU_HOST_D2H a pipeline has no D2H path until its first call, which times the
+    copy engine against the device stores (32 MiB each) and keeps one; the call's results are
+    the oracle's whichever it keeps."""
+    from oracle import oracle as O
+    T = _T()
+    from tlslite_amd import _native as N
+    from tlslite_amd.device import DeviceBuffer
+    from tlslite_amd.recordlayer import HostSealPipeline
+    from tlslite_amd.state import pack_states
+    monkeypatch.delenv("TLSGPU_HOST_D2H", raising=False)
+    rng = np.random.default_rng(99)
+    nconn = 64
+    readers, oreaders, streams = _streams(T, O, "AES128-SHA", (3, 3), nconn, rng)
+    rx, pt, offs, keep = _arena(streams, rng, True)
+    spans = (N.Span * nconn)()
+    for i, sp in enumerate(spans):
+        sp.off, sp.len, sp.state = offs[i], len(streams[i]), i
+    d_states = DeviceBuffer(pack_states(readers).size)
+    d_states.upload(pack_states(readers))
+    full = sum(len(O.frame(d)[0]) for d in streams)
+    want = _expect(O, streams, oreaders, full + 3)
+    with HostSealPipeline(16 << 10, 3) as hp:
+        assert hp.d2h_path is None
+        res = hp.open(rx, spans, pt, d_states, readers[0].variant, max_records=full + 3)
+        assert hp.d2h_path in ("engine", "stores")
+    ch = np.frombuffer(res["chains"], dtype=np.uint32).reshape(nconn, 4)
+    recs = np.frombuffer(res["records"], dtype=np.uint8).reshape(-1, 24)
+    for ci, (fst, consumed, rows) in enumerate(want):
+        assert int(res["frame_status"][ci]) == fst
+        for k, (t, boff, blen, st, p) in enumerate(rows):
+            r = int(ch[ci, 1]) + k
+            if st >= 0:
+                ct_off = int(recs[r, 0:8].view(np.uint64)[0])
+                assert pt[ct_off:ct_off + st].tobytes() == p, (ci, k)

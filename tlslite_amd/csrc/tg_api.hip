@@ -659,15 +659,15 @@ static int choose_d2h_path(tlsgpu_host_pipeline p) {
     const size_t n = (size_t)32 << 20;
     DevBuf src;
     PinBuf dst;
-    TG_HIP(src.ensure(n));
-    TG_HIP(dst.ensure(n));
-    uint8_t* dd = host_store_ptr(dst.p);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
     float best[2] = {1e30f, 1e30f};
-    if (dd) {
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        TG_HIP(hipEventCreate(&e0));
-        TG_HIP(hipEventCreate(&e1));
-        hipError_t e = hipMemsetAsync(src.p, 0, n, p->d2h);
+    hipError_t e = src.ensure(n);
+    if (e == hipSuccess) e = dst.ensure(n);
+    uint8_t* dd = e == hipSuccess ? host_store_ptr(dst.p) : nullptr;
+    if (dd) {  // else the copy engine (no device address for the stores)
+        e = hipEventCreate(&e0);
+        if (e == hipSuccess) e = hipEventCreate(&e1);
+        if (e == hipSuccess) e = hipMemsetAsync(src.p, 0, n, p->d2h);
         for (int rep = 0; rep < 4 && e == hipSuccess; rep++)
             for (int k = 0; k < 2 && e == hipSuccess; k++) {
                 e = hipEventRecord(e0, p->d2h);
@@ -680,12 +680,13 @@ static int choose_d2h_path(tlsgpu_host_pipeline p) {
                 if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
                 if (e == hipSuccess && rep) best[k] = ms < best[k] ? ms : best[k];
             }
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
-        if (e != hipSuccess) return fail_hip(e, "host pipeline D2H calibration");
     }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (e == hipSuccess) e = hipStreamSynchronize(p->d2h);  // before the buffers go
     src.release();
     dst.release();
+    if (e != hipSuccess) return fail_hip(e, "host pipeline D2H calibration");
     p->d2h_path = best[1] * 1.25f < best[0] ? 1 : 0;
     return 0;
 }
