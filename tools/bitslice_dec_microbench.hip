@@ -158,27 +158,40 @@ __host__ __device__ __forceinline__ void bs_transpose32(uint32_t* a) {
 // ciphertext blocks (reloaded: an L2 hit), store.  rk[0..10] the encryption round keys,
 // wave-uniform (the record's).  Rounds 9..2 as pairs in a loop (two rounds of code, ~45 KB), the
 // last two after it.
+// STRIDED: lane l of a wave takes blocks base + l + 64 j (each load / store instruction moves one
+// contiguous KiB) instead of base + 32 l + j (each lane its own 512 B)
+template <bool STRIDED>
 __global__ void __launch_bounds__(64) bcbc_kernel(const uint32_t* __restrict__ rk, const uint4* __restrict__ ct,
                                                   uint4* __restrict__ pt, uint64_t* __restrict__ cyc, int iters,
                                                   const uint32_t* done, uint32_t stop, uint32_t* __restrict__ iters_done) {
     const uint32_t gid = blockIdx.x * 64 + threadIdx.x;
-    const uint4* c = ct + (size_t)gid * 32;
-    uint4* o = pt + (size_t)gid * 32;
+    const size_t b0 = STRIDED ? (size_t)blockIdx.x * 2048 + threadIdx.x : (size_t)gid * 32;
+    constexpr size_t BS = STRIDED ? 64 : 1;  // block stride between a lane's blocks
+    const uint4* c = ct + b0;
+    uint4* o = pt + b0;
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     int it = 0;
     for (; it < iters; it++) {
         if (stop && __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= stop) break;
         uint32_t p[128], q[128];
+        // the block addresses are loop-invariant: kept opaque per iteration, or the compiler
+        // hoists all 96 of them (strided layout: 1-KiB steps, no immediate offsets) into VGPRs
+        uintptr_t cb = reinterpret_cast<uintptr_t>(c), ob = reinterpret_cast<uintptr_t>(o);
+        asm volatile("" : "+v"(cb), "+v"(ob));
+        const uint4* c = reinterpret_cast<const uint4*>(cb);
+        uint4* o = reinterpret_cast<uint4*>(ob);
         // word w of the 32 blocks XOR the last round key's word w (the transpose is linear, and
         // plane masks of a loop-invariant key would be hoisted into 128 VGPRs), then its transpose
-        const uint32_t* cw = reinterpret_cast<const uint32_t*>(c);
+        {
+            const uint32_t* cw = reinterpret_cast<const uint32_t*>(c);
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
+            for (int w = 0; w < 4; w++) {
 #pragma unroll
-            for (int j = 0; j < 32; j++) p[32 * w + j] = cw[4 * j + w] ^ rk[40 + w];  // round-10 key, pre-transpose
-            __builtin_amdgcn_sched_barrier(0);
-            bs_transpose32(p + 32 * w);
-            __builtin_amdgcn_sched_barrier(0);
+                for (int j = 0; j < 32; j++) p[32 * w + j] = cw[4 * BS * j + w] ^ rk[40 + w];  // round-10 key, pre-transpose
+                __builtin_amdgcn_sched_barrier(0);
+                bs_transpose32(p + 32 * w);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         }
 #pragma unroll 1
         for (int r = 9; r >= 3; r -= 2) {
@@ -196,8 +209,9 @@ __global__ void __launch_bounds__(64) bcbc_kernel(const uint32_t* __restrict__ r
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int j = 0; j < 32; j++) {
-            const uint4 v = j ? c[j - 1] : (gid ? c[-1] : make_uint4(0, 0, 0, 0));
-            o[j] = make_uint4(p[j] ^ v.x, p[32 + j] ^ v.y, p[64 + j] ^ v.z, p[96 + j] ^ v.w);
+            const size_t blk = b0 + BS * j;  // predecessor block blk - 1 (block 0: a zero IV)
+            const uint4 v = blk ? c[(ptrdiff_t)(BS * j) - 1] : make_uint4(0, 0, 0, 0);
+            o[BS * j] = make_uint4(p[j] ^ v.x, p[32 + j] ^ v.y, p[64 + j] ^ v.z, p[96 + j] ^ v.w);
             if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);  // at most 8 reloads in flight
         }
     }
@@ -368,6 +382,7 @@ static void expand128(const uint8_t key[16], uint32_t rk[44], const uint8_t* sbo
 
 // The bitsliced CBC decrypt on real data: alone (bsw waves per CU) or beside the T kernel.
 // Checked against FIPS-197 C.1 (block 0) and a byte-wise InvCipher + CBC of two lanes' blocks.
+template <bool STRIDED>
 static void run_cbc(const char* name, bool t, int bsw, const uint32_t* d_dk, int cus, int it_t, int it_b,
                     const uint8_t* sbox, const uint8_t* isbox) {
     streams();
@@ -412,7 +427,7 @@ static void run_cbc(const char* name, bool t, int bsw, const uint32_t* d_dk, int
         (void)hipStreamWaitEvent(sb, e0, 0);
         if (nt) hipLaunchKernelGGL(t_kernel, dim3(cus), dim3(1024), AES_DEC_LDS_BYTES, sa, d_dk, t_out, t_cyc,
                                    pass ? it_t : 2, done + 32 * pass);
-        hipLaunchKernelGGL(bcbc_kernel, dim3(nb), dim3(64), 0, sb, (const uint32_t*)d_rk, (const uint4*)d_ct, d_pt,
+        hipLaunchKernelGGL(bcbc_kernel<STRIDED>, dim3(nb), dim3(64), 0, sb, (const uint32_t*)d_rk, (const uint4*)d_ct, d_pt,
                            b_cyc, pass ? b_cap : 1, (const uint32_t*)(done + 32 * pass), stop, b_it);
         (void)hipEventRecord(ea, sa);
         (void)hipEventRecord(eb, sb);
@@ -490,10 +505,14 @@ int main(int argc, char** argv) {
     run("T+B4", true, 4, d_dk, cus, it_t, it_b, dk, isbox, true);
     run("T+B8", true, 8, d_dk, cus, it_t, it_b, dk, isbox, false);
     const int it_c = argc > 3 ? atoi(argv[3]) : 40;  // CBC-B alone: passes over the lane's 32 blocks
-    run_cbc("CBC-B4", false, 4, d_dk, cus, it_t, it_c, sbox, isbox);
-    run_cbc("CBC-B8", false, 8, d_dk, cus, it_t, it_c, sbox, isbox);
-    run_cbc("CBC-B12", false, 12, d_dk, cus, it_t, it_c, sbox, isbox);
-    run_cbc("T+CBC-B4", true, 4, d_dk, cus, it_t, it_c, sbox, isbox);
-    run_cbc("T+CBC-B8", true, 8, d_dk, cus, it_t, it_c, sbox, isbox);
+    run_cbc<false>("CBC-B4", false, 4, d_dk, cus, it_t, it_c, sbox, isbox);
+    run_cbc<false>("CBC-B8", false, 8, d_dk, cus, it_t, it_c, sbox, isbox);
+    run_cbc<false>("CBC-B12", false, 12, d_dk, cus, it_t, it_c, sbox, isbox);
+    run_cbc<false>("T+CBC-B4", true, 4, d_dk, cus, it_t, it_c, sbox, isbox);
+    run_cbc<false>("T+CBC-B8", true, 8, d_dk, cus, it_t, it_c, sbox, isbox);
+    run_cbc<true>("CBC-S8", false, 8, d_dk, cus, it_t, it_c, sbox, isbox);
+    run_cbc<true>("CBC-S12", false, 12, d_dk, cus, it_t, it_c, sbox, isbox);
+    run_cbc<true>("T+CBC-S4", true, 4, d_dk, cus, it_t, it_c, sbox, isbox);
+    run_cbc<true>("T+CBC-S8", true, 8, d_dk, cus, it_t, it_c, sbox, isbox);
     return 0;
 }
