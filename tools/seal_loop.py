@@ -1,0 +1,38 @@
+"""Seal the cfg2 batch through the seal pipeline back to back for --seconds (diagnostic for
+tools/clock_watch.sh: clock and power under sustained load); prints GiB/s per --block steps (each block bracketed by synchronizations, as bench.py's timed region)."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=8.0)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--block", type=int, default=200, help="steps between synchronizations")
+    a = ap.parse_args()
+    from tlslite_amd import workloads as W
+    from tlslite_amd.device import synchronize
+    from tlslite_amd.recordlayer import SealPipeline
+    wl = W.CONFIGS[a.config]()
+    wl.to_device()
+    synchronize()
+    pipe = SealPipeline(wl.n_records)
+    t_end = time.perf_counter() + a.seconds
+    while time.perf_counter() < t_end:
+        t0 = time.perf_counter()
+        for _ in range(a.block):
+            wl.launch(pipeline=pipe)
+        pipe.synchronize()
+        synchronize()
+        dt = time.perf_counter() - t0
+        print("%.3f %.1f GiB/s" % (time.time(), a.block * wl.plaintext_total / (1 << 30) / dt), flush=True)
+    pipe.close()
+    wl.free()
+
+
+if __name__ == "__main__":
+    main()
