@@ -57,9 +57,10 @@ def parse():
     ap.add_argument("--pt-align", type=int, default=16,
                     help="plaintext slot alignment of the workload (16: packed, as generic callers lay records out; "
                          "128: every record on a cache line)")
-    # defaults: 500 + 500 steps (~1 s of GPU time for cfg2): under sustained load the GPU's clocks settle
-    # ~4 % above what a 5-step warmup + 50-step run sees (profiles/r03/warmup_steps.txt); cfg4 (~0.12 s per
-    # step): 2 + 10.  Explicit --steps / --warmup are used as given.
+    # defaults: 500 + 500 steps (~1 s of GPU time for cfg2): sustained load, ~4 % above what a 5-step
+    # warmup + 50-step run sees (profiles/r03/warmup_steps.txt; a fresh process's first seal steps run
+    # slower and a short timed region pays the pipeline's fill: DESIGN.md section 4, profiles/r06/clock);
+    # cfg4 (~0.12 s per step): 2 + 10.  Explicit --steps / --warmup are used as given.
     ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=None)
     ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5"])
@@ -1256,7 +1257,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": wl.dominant_kernel(), "kernel_avg_ms": round(avg_ms, 4),
                          # the timed steps' kernel times in order: a short run's first steps run
-                         # at the clocks of a GPU that has just started working
+                         # slower than later ones ("Short runs")
                          # the timed steps whose kernel the events bracket: k % every == every // 2
                          "kernel_events": {"every": args.kernel_events_every, "steps": len(ev_steps),
                                            "first": ev_steps[0], "last": ev_steps[-1],
