@@ -13,6 +13,11 @@ def main():
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--block", type=int, default=200, help="steps between synchronizations")
+    ap.add_argument("--pipe-first", action="store_true", help="create the pipeline before --pre's work")
+    ap.add_argument("--pre-n", type=int, default=40, help="seal_dev calls of --pre dev")
+    ap.add_argument("--pre", default="none", choices=["none", "dev", "fill"],
+                    help="before the loop: none; 'dev' 40 tlsgpu_seal_dev calls; 'fill' ~100 ms of an unrelated "
+                         "kernel (fill_pattern over a 4 GiB buffer, 25 times)")
     a = ap.parse_args()
     from tlslite_amd import workloads as W
     from tlslite_amd.device import synchronize
@@ -20,7 +25,20 @@ def main():
     wl = W.CONFIGS[a.config]()
     wl.to_device()
     synchronize()
-    pipe = SealPipeline(wl.n_records)
+    pipe = SealPipeline(wl.n_records) if a.pipe_first else None
+    if a.pre == "dev":
+        for _ in range(a.pre_n):
+            wl.launch()
+        synchronize()
+    elif a.pre == "fill":
+        from tlslite_amd import _native as N
+        from tlslite_amd.device import DeviceBuffer
+        buf = DeviceBuffer(4 << 30)
+        for k in range(25):
+            N.call("tlsgpu_fill_pattern", buf.ptr, buf.nbytes, k, 0, None)
+        synchronize()
+        buf.free()
+    pipe = pipe or SealPipeline(wl.n_records)
     t_end = time.perf_counter() + a.seconds
     while time.perf_counter() < t_end:
         t0 = time.perf_counter()
