@@ -1046,7 +1046,7 @@ def main():
         wl.reset_states(stream)
 
     # the seal pipeline (its streams, events and workspaces) is set up before the legs below, so
-    # no allocation gap idles the GPU between them and the warmup steps
+    # no host-side setup idles the GPU between their seals and the warmup steps
     from tlslite_amd.recordlayer import SealPipeline
     pipe = SealPipeline(wl.n_records)
     n_state_launches = 0  # seals applied to the connection states since the last reset

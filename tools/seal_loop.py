@@ -14,6 +14,8 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--block", type=int, default=200, help="steps between synchronizations")
     ap.add_argument("--pipe-first", action="store_true", help="create the pipeline before --pre's work")
+    ap.add_argument("--alloc-between", type=int, default=0,
+                    help="MiB to hipMalloc and free between blocks (0: none): does an allocation slow the next block?")
     ap.add_argument("--pre-n", type=int, default=40, help="seal_dev calls of --pre dev")
     ap.add_argument("--pre", default="none", choices=["none", "dev", "fill"],
                     help="before the loop: none; 'dev' 40 tlsgpu_seal_dev calls; 'fill' ~100 ms of an unrelated "
@@ -40,7 +42,13 @@ def main():
         buf.free()
     pipe = pipe or SealPipeline(wl.n_records)
     t_end = time.perf_counter() + a.seconds
+    from tlslite_amd.device import DeviceBuffer
+    nblk = 0
     while time.perf_counter() < t_end:
+        if a.alloc_between and nblk % 4 == 3:
+            DeviceBuffer(a.alloc_between << 20).free()
+            print("-- allocated and freed %d MiB" % a.alloc_between, flush=True)
+        nblk += 1
         t0 = time.perf_counter()
         for _ in range(a.block):
             wl.launch(pipeline=pipe)
