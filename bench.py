@@ -515,7 +515,7 @@ def host_open_rate(wl, link=None, chunk=64 << 20, depth=3):
     return out
 
 
-def gpu_warm(call, sync, min_ms=40.0, max_calls=40):
+def gpu_warm(call, sync, min_ms=40.0, max_calls=400):
     """Untimed calls back to back (synchronised every 4) until min_ms of them have run: a side leg
     measured after seconds of host work would otherwise time a GPU waking from its idle clock
     ("Short runs")."""
@@ -705,6 +705,13 @@ def frame_rate(wl, stream, steps):
     ws = DeviceBuffer(frame_workspace_bytes(n))
     d_ost, d_ows = DeviceBuffer(4 * n), DeviceBuffer(wl.d_ows[0].nbytes)
     fms, foms = [], []
+
+    def warm_call():
+        N.call("tlsgpu_memcpy_d2d", wl.d_ostates.ptr, wl.d_states0.ptr, wl.d_ostates.nbytes, stream.handle)
+        frame_dev(wl.d_wire, d_sp, n, d_r, n, d_c, d_cons, d_st, d_tot, workspace=ws, s=stream)
+        open_dev(d_c, n, d_r, n, wl.d_wire, wl.d_opt, wl.d_ostates, d_ost, var, d_ows, stream)
+
+    gpu_warm(warm_call, stream.synchronize)
     for it in range(max(2, min(steps, 20)) + 1):
         a, b, c = Event(), Event(), Event()
         N.call("tlsgpu_memcpy_d2d", wl.d_ostates.ptr, wl.d_states0.ptr, wl.d_ostates.nbytes, stream.handle)
@@ -862,6 +869,8 @@ def derive_rate(stream, nconn=4096, steps=10):
     ws, rs = DeviceBuffer(nconn * N.CONN_STATE_BYTES), DeviceBuffer(nconn * N.CONN_STATE_BYTES)
     kb, st = DeviceBuffer(nconn * N.KEY_BLOCK_MAX), DeviceBuffer(4 * nconn)
     ms = []
+    gpu_warm(lambda: N.call("tlsgpu_derive_states_dev", dd.ptr, nconn, ws.ptr, rs.ptr, None, kb.ptr, st.ptr,
+                            stream.handle), stream.synchronize)
     for it in range(steps + 1):
         a, b = Event(), Event()
         a.record(stream)
