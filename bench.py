@@ -1120,9 +1120,10 @@ def main():
     for _ in range(args.warmup):
         wl.launch(pipeline=pipe)
     n_state_launches += args.warmup
-    pipe.synchronize()
-    synchronize()
+    # the ranks meet while their GPUs still run the warmup steps, then each waits for its own:
+    # a barrier over TCP between two synchronisations would idle every GPU for its duration
     D.barrier()
+    pipe.synchronize()
     synchronize()
     if conc:
         for _ in range(args.warmup):
