@@ -634,10 +634,14 @@ def open_concurrent_rate(wl, calls, nstreams=2, D=None, ranks_per_device=1):
                     open_dev(d_ch, nch, wl.d_orecs, wl.n_records, wl.d_wire, pts[0], wl.d_ostates, stat[0], var,
                              wss[0][j], streams[0])
             gpu_warm(warm_call, streams[0].synchronize)
+            for _ in range(4):  # still running while the ranks meet below
+                warm_call()
         except Exception as e:
             err = e
     if D is not None:
         D.barrier()
+    for s_ in streams:
+        s_.synchronize()
     t0 = time.perf_counter()
     try:
         for k in range(calls):
