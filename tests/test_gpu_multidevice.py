@@ -89,3 +89,42 @@ def test_calls_on_another_devices_stream():
     a.free()
     b.free()
     set_device(0)
+
+
+def test_host_pipeline_on_another_device():
+    """A host pipeline created on device 1 and called with device 0 current seals and opens on
+    device 1 (its streams and buffers live there; tlsgpu_host_pipeline_* switch to it for the
+    call and restore the caller's device), results equal to the device-resident path."""
+    from tlslite_amd import _native as N
+    from tlslite_amd.constants import ContentType
+    import ctypes
+    from tlslite_amd.device import PinnedBuffer, device_count, set_device, synchronize
+    from tlslite_amd.recordlayer import HostSealPipeline, make_chains, make_records
+    if device_count() < 2:
+        pytest.skip("one GPU visible: the cross-device case needs two")
+    wl, s = _batch(1, 61)
+    wl.launch()
+    synchronize()
+    ref = wl.d_wire.download()
+    var = wl.launches[0][0]
+    recs = make_records(wl.pt_off, wl.wire_off, wl.pt_len, ContentType.application_data, 0)
+    chains = make_chains(np.arange(wl.n_chains, dtype=np.uint32), wl.chain_first, wl.chain_count)
+    pin_pt, pin_wire = PinnedBuffer(wl.pt_bytes), PinnedBuffer(wl.wire_bytes)
+    wl.d_pt.download(out=pin_pt.array[: wl.pt_bytes])
+    pin_wire.array[:] = 0
+    lens = np.zeros(wl.n_records, dtype=np.int32)
+    wl.reset_states()
+    synchronize()
+    hp = HostSealPipeline(64 << 10, 3)  # created with device 1 current
+    set_device(0)
+    hp.seal(chains, recs, pin_pt.array[: wl.pt_bytes], pin_wire.array[: wl.wire_bytes], wl.d_states, lens, var)
+    cur = ctypes.c_int(-1)
+    N.call("tlsgpu_get_device", ctypes.byref(cur))
+    assert cur.value == 0
+    assert np.array_equal(pin_wire.array[: wl.wire_bytes], ref)
+    hp.close()
+    pin_pt.free()
+    pin_wire.free()
+    set_device(1)
+    wl.free()
+    set_device(0)

@@ -60,6 +60,27 @@ int ks_fail(int code) { return code ? fail(TLSGPU_EINVAL, KS_MSG[code]) : 0; }
 inline ConnState* S(tlsgpu_conn_state* p) { return reinterpret_cast<ConnState*>(p); }
 inline const ConnState* S(const tlsgpu_conn_state* p) { return reinterpret_cast<const ConnState*>(p); }
 inline hipStream_t HS(tlsgpu_stream s) { return reinterpret_cast<hipStream_t>(s); }
+// A pipeline's calls run on the device it was created on (its streams, events and buffers live
+// there) whatever device the calling thread has current; the caller's device is restored after.
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            (void)hipGetLastError();
+            prev = -1;
+            return;
+        }
+        if (prev == dev) {
+            prev = -1;
+        } else if (hipSetDevice(dev) != hipSuccess) {
+            (void)hipGetLastError();
+            prev = -1;
+        }
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
 
 hipError_t own_release_stream(hipStream_t s);
 
@@ -449,6 +470,7 @@ int tlsgpu_pipeline_create(tlsgpu_pipeline* out, uint32_t max_records) {
 
 int tlsgpu_pipeline_destroy(tlsgpu_pipeline p) {
     if (!p) return 0;
+    DeviceScope scope_(p->dev);
     (void)hipStreamSynchronize(p->mac_s);
     (void)hipStreamSynchronize(p->cbc_s);
     for (int i = 0; i < PIPE_WS; i++) {
@@ -473,6 +495,7 @@ int tlsgpu_pipeline_seal(tlsgpu_pipeline p, const tlsgpu_chain* chains, uint32_t
                          uint8_t* wire, size_t wire_bytes, tlsgpu_conn_state* states, uint32_t nstates,
                          int32_t* wire_len, uint32_t variant, tlsgpu_event cipher_start, tlsgpu_event cipher_stop) {
     if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
+    DeviceScope scope_(p->dev);
     if (nchains == 0) return 0;
     if (!chains || !records || !pt || !wire || !states || !wire_len) return fail(TLSGPU_EINVAL, "null pointer");
     if (seal_workspace_bytes(nrecords) > p->ws_bytes) return fail(TLSGPU_EINVAL, "nrecords > pipeline max_records");
@@ -765,6 +788,7 @@ int tlsgpu_host_pipeline_create(tlsgpu_host_pipeline* out, size_t chunk_bytes, i
 
 int tlsgpu_host_pipeline_destroy(tlsgpu_host_pipeline p) {
     if (!p) return 0;
+    DeviceScope scope_(p->dev);
     for (hipStream_t s : {p->h2d, p->mac, p->cbc, p->d2h, p->frs}) (void)hipStreamSynchronize(s);
     p->pt.release();
     p->wire.release();
@@ -822,6 +846,7 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain* chains
                               size_t pt_bytes, uint8_t* wire_host, size_t wire_bytes, tlsgpu_conn_state* states,
                               uint32_t nstates, int32_t* wire_len_host, uint32_t variant) {
     if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
+    DeviceScope scope_(p->dev);
     if (nchains == 0) return 0;
     if (!chains || !records || !pt_host || !wire_host || !states || !wire_len_host)
         return fail(TLSGPU_EINVAL, "null pointer");
@@ -1025,6 +1050,7 @@ int tlsgpu_host_pipeline_open(tlsgpu_host_pipeline p, const uint8_t* rx_host, si
                               uint32_t* consumed_host, int32_t* frame_status_host, int32_t* status_host,
                               uint32_t* total_host) {
     if (!p) return fail(TLSGPU_EINVAL, "null pipeline");
+    DeviceScope scope_(p->dev);
     if (!total_host) return fail(TLSGPU_EINVAL, "null pointer");
     *total_host = 0;
     if (n == 0) return 0;
