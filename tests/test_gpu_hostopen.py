@@ -178,7 +178,8 @@ def test_host_pipeline_open_vs_oracle(suite, version, pinned, depth, chunk, cut,
 def test_host_store_copies_exactly():
     """tlsgpu_host_store (a D2H copy by the GPU's own stores, the host pipelines' other D2H path):
     every byte of ranges with ragged heads and tails lands, nothing around them is written, a
-    destination that is not pinned or differs mod 16 is refused; and a fresh pipeline's first
+    destination that is not pinned or differs mod 16, or a source that is not device memory, is
+    refused; and a fresh pipeline's first
     call chooses a path (calibration) without changing its results."""
     _T()
     from tlslite_amd import _native as N
@@ -202,6 +203,8 @@ def test_host_store_copies_exactly():
     pageable = np.zeros(64, dtype=np.uint8)
     with pytest.raises(N.TLSGPUError):
         N.call("tlsgpu_host_store", pageable.ctypes.data, d.addr, 64, s.handle)
+    with pytest.raises(N.TLSGPUError):  # the source must be device memory
+        N.call("tlsgpu_host_store", h.ptr.value, h.ptr.value + 4096, 64, s.handle)
     d.free()
     h.free()
 

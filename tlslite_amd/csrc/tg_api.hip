@@ -733,6 +733,11 @@ int tlsgpu_host_store(void* dst_host, const void* src_dev, size_t bytes, tlsgpu_
     if (!dst_host || !src_dev) return fail(TLSGPU_EINVAL, "null pointer");
     uint8_t* dd = host_store_ptr(dst_host);
     if (!dd) return fail(TLSGPU_EINVAL, "destination is not pinned host memory the device can store into");
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, src_dev) != hipSuccess || a.type != hipMemoryTypeDevice) {
+        (void)hipGetLastError();
+        return fail(TLSGPU_EINVAL, "source is not device memory");
+    }
     if (((uintptr_t)dd ^ (uintptr_t)src_dev) & 15) return fail(TLSGPU_EINVAL, "source and destination differ mod 16");
     hipError_t e = launch_host_store(static_cast<const uint8_t*>(src_dev), dd, bytes, HS(s));
     if (e != hipSuccess) return fail_hip(e, "host store launch");
