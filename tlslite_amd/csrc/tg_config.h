@@ -34,6 +34,9 @@ constexpr int CFG_PAIR_G1 = 8;
 constexpr int CFG_PAIR_GM = 4;
 // seal pipeline: workspaces in rotation (the MAC stream may run PIPE_WS - 1 calls ahead)
 constexpr int CFG_PIPE_WS = 3;
+// open MAC: batches of at most this many records per CU take the cooperative-load, one-wave-
+// workgroup form (the receive pipeline's sub-batches, round 6)
+constexpr int CFG_OPEN_MAC_COOP_PER_CU = 64;
 // host seal pipeline, pinned arenas: 0 = every sub-batch's H2D copy enqueued at once; L > 0 =
 // sub-batch i's H2D copy waits until sub-batch i - L's D2H copy may start (its seal is done),
 // so the H2D direction cannot run far ahead of the D2H one (experiment knob, round 6)

@@ -805,7 +805,7 @@ static hipError_t launch_open_split(const tlsgpu_chain* chains, uint32_t nchains
     // as many CUs as there are waves (four 256-lane workgroups put a 1,024-record batch on 4
     // CUs, where the concurrent sub-batches' MAC and framing kernels land too: 1.4 ms in the
     // pipeline against 0.35 ms alone, tools/open_mac_probe.py)
-    const bool coop = nrecords <= 64u * ncu;
+    const bool coop = nrecords <= (uint32_t)CFG_OPEN_MAC_COOP_PER_CU * ncu;
     auto mac = [&](uint32_t c0, uint32_t c1, hipStream_t s, int part = -1, int nparts = 0) {
         if (coop)
             hipLaunchKernelGGL((open_mac_kernel<MAC, SSL3, BS, true>), dim3((nrecords + 63) / 64), dim3(64), 0, s, recs,

@@ -44,6 +44,9 @@
 #ifndef TG_AB_H2D_LEAD
 #define TG_AB_H2D_LEAD 0
 #endif
+#ifndef TG_AB_OPEN_COOP
+#define TG_AB_OPEN_COOP 64
+#endif
 namespace tg {
 constexpr int CFG_CBC_WAVES = TG_AB_CBC_WAVES;
 constexpr int CFG_MAC_PRIO = TG_AB_MAC_PRIO;
@@ -58,4 +61,5 @@ constexpr int CFG_PAIR_G1 = TG_AB_PAIR_G1;
 constexpr int CFG_PAIR_GM = TG_AB_PAIR_GM;
 constexpr int CFG_PIPE_WS = TG_AB_PIPE_WS;
 constexpr int CFG_HOST_H2D_LEAD = TG_AB_H2D_LEAD;
+constexpr int CFG_OPEN_MAC_COOP_PER_CU = TG_AB_OPEN_COOP;
 }  // namespace tg
