@@ -187,3 +187,29 @@ def test_hip_error_in_a_leg_fails_the_run():
     # N > 1: a rank's failure nested in the aggregated leg
     agg = {"error": "open leg failed on rank(s) [1]", "ranks": [{"value": 1.0}, hip]}
     assert bench.hip_failures({"open": agg, "host_inclusive": None}) == ["open"]
+
+
+def test_link_ceiling_takes_the_better_d2h_path():
+    """The host legs price their PCIe ceiling with the better of the pipelines' two D2H paths
+    (copy engine or device stores): the engine's rates when it is the
+    faster one, the stores' in a process where the engine's D2H runs slow."""
+    import bench
+    good = {"h2d": 57.5, "d2h": 57.0, "both": 97.1, "d2h_stores": 54.6, "both_stores": 85.4}
+    slow = {"h2d": 57.5, "d2h": 30.0, "both": 57.0, "d2h_stores": 54.7, "both_stores": 87.2}
+    assert bench.link_best(good) == (57.0, 97.1)
+    assert bench.link_best(slow) == (54.7, 87.2)
+    assert bench.link_best({"h2d": 57.5, "d2h": 57.0, "both": 97.1}) == (57.0, 97.1)  # no stores probe
+
+
+def test_gpu_warm_runs_until_its_time_or_call_budget():
+    """The side legs' warm-up burst: calls in groups of four, each group synchronised, until
+    min_ms have passed or max_calls were made."""
+    import time
+    import bench
+    calls, syncs = [], []
+    n = bench.gpu_warm(lambda: calls.append(1), lambda: syncs.append(1), min_ms=1e9, max_calls=12)
+    assert n == 12 and len(calls) == 12 and len(syncs) == 3
+    calls.clear()
+    t0 = time.perf_counter()
+    n = bench.gpu_warm(lambda: (calls.append(1), time.sleep(0.002)), lambda: None, min_ms=20.0, max_calls=400)
+    assert 8 <= n <= 16 and (time.perf_counter() - t0) * 1e3 >= 20.0
