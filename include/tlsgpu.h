@@ -331,9 +331,9 @@ int tlsgpu_host_pipeline_seal(tlsgpu_host_pipeline p, const tlsgpu_chain *chains
                               uint32_t nstates, int32_t *wire_len_host, uint32_t variant);
 /* The host pipelines' large D2H copies (wire ranges, opened plaintext) go by the copy engine or
  * by the GPU's own stores into the pinned destination (tlsgpu_host_store's kernel): each pipeline
- * times both on its first call (32 MiB, ~3 ms) and keeps the stores only when they are >= 1.25x
- * faster -- in some processes the engine's D2H runs at about half its usual rate while the
- * stores do not.  TLSGPU_HOST_D2H=engine|kernel in the environment
+ * times them on its first call (32 MiB, ~4 ms) and keeps the stores only when the engine's D2H
+ * runs below 0.7x its H2D rate and the stores are >= 1.5x faster -- in some processes the
+ * engine's D2H runs at about half its usual rate while the stores do not.  TLSGPU_HOST_D2H=engine|kernel in the environment
  * forces a path.  *path: -1 not chosen yet, 0 copy engine, 1 device stores. */
 int tlsgpu_host_pipeline_d2h_path(tlsgpu_host_pipeline p, int *path);
 /* D2H copy by device stores, async on s: dst_host is pinned host memory (tlsgpu_host_alloc) at

@@ -666,8 +666,8 @@ struct tlsgpu_host_pipeline_s {
 // GPU's own stores (host_store_kernel).  On most boxes the engine is the faster one beside the
 // H2D copies (56 + 48 GB/s against 43 + 50), but in about one process in four its D2H runs at
 // 30 GB/s where the stores still reach 55 (profiles/r06/hostpipe/NOTES.md).  So each pipeline
-// times both once, on its first call (32 MiB each, best of 3, ~3 ms), and takes the stores only
-// when they are >= 1.25x faster.  TLSGPU_HOST_D2H=engine|kernel forces a path (tests).
+// times them once, on its first call (32 MiB each, best of 3, ~4 ms), and takes the stores only
+// when the engine's D2H runs at < 0.7x its own H2D rate and the stores are >= 1.5x faster.  TLSGPU_HOST_D2H=engine|kernel forces a path (tests).
 static int choose_d2h_path(tlsgpu_host_pipeline p) {
     if (p->d2h_path >= 0) return 0;
     const char* env = getenv("TLSGPU_HOST_D2H");
@@ -683,7 +683,7 @@ static int choose_d2h_path(tlsgpu_host_pipeline p) {
     DevBuf src;
     PinBuf dst;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    float best[2] = {1e30f, 1e30f};
+    float best[3] = {1e30f, 1e30f, 1e30f};  // engine D2H, stores D2H, engine H2D (ms for n bytes)
     hipError_t e = src.ensure(n);
     if (e == hipSuccess) e = dst.ensure(n);
     uint8_t* dd = e == hipSuccess ? host_store_ptr(dst.p) : nullptr;
@@ -692,11 +692,12 @@ static int choose_d2h_path(tlsgpu_host_pipeline p) {
         if (e == hipSuccess) e = hipEventCreate(&e1);
         if (e == hipSuccess) e = hipMemsetAsync(src.p, 0, n, p->d2h);
         for (int rep = 0; rep < 4 && e == hipSuccess; rep++)
-            for (int k = 0; k < 2 && e == hipSuccess; k++) {
+            for (int k = 0; k < 3 && e == hipSuccess; k++) {
                 e = hipEventRecord(e0, p->d2h);
                 if (e == hipSuccess)
-                    e = k ? launch_host_store(src.u8(), dd, n, p->d2h)
-                          : hipMemcpyAsync(dst.p, src.p, n, hipMemcpyDeviceToHost, p->d2h);
+                    e = k == 1   ? launch_host_store(src.u8(), dd, n, p->d2h)
+                        : k == 0 ? hipMemcpyAsync(dst.p, src.p, n, hipMemcpyDeviceToHost, p->d2h)
+                                 : hipMemcpyAsync(src.p, dst.p, n, hipMemcpyHostToDevice, p->d2h);
                 if (e == hipSuccess) e = hipEventRecord(e1, p->d2h);
                 if (e == hipSuccess) e = hipEventSynchronize(e1);
                 float ms = 0;
@@ -710,7 +711,11 @@ static int choose_d2h_path(tlsgpu_host_pipeline p) {
     src.release();
     dst.release();
     if (e != hipSuccess) return fail_hip(e, "host pipeline D2H calibration");
-    p->d2h_path = best[1] * 1.25f < best[0] ? 1 : 0;
+    // The anomaly the stores path is for: the engine's D2H at about half its H2D rate (30 vs 57
+    // GB/s) while the stores reach 55.  Both conditions, so that copies of other processes on a
+    // shared link -- which slow the engine's two directions alike -- do not pick the stores (8
+    // ranks on one GPU: engine 40.8 vs stores 33.5 GiB/s, profiles/r06/hostpipe/NOTES.md).
+    p->d2h_path = (best[0] > 1.4f * best[2] && best[1] * 1.5f < best[0]) ? 1 : 0;
     return 0;
 }
 
