@@ -81,9 +81,10 @@ def parse():
                     help="force the open path's split form (tlsgpu_set_open_parts; default: the library's choice)")
     ap.add_argument("--traffic", default=None, help="JSON with PMC-derived HBM bytes per launch")
     ap.add_argument("--kernel-events-every", type=int, default=None,
-                    help="bracket the dominant kernel with HIP timing events on every M-th timed step (the steps "
-                         "k with k %% M == M // 2); each pair of event records costs ~25 us of the cipher stream's "
-                         "time per step (DESIGN.md section 4).  Default 4 (cfg4, cfg5: 1)")
+                    help="time the dominant kernel with HIP events on every M-th timed step (the steps k with "
+                         "k %% M == M // 2): AES suites, the cipher kernel's own dispatch events (hipExtLaunchKernelGGL); "
+                         "RC4 / 3DES-only batches, event records around the call (~25 us each pair, DESIGN.md "
+                         "section 4).  Default 4 (cfg4, cfg5: 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="minimum CPU time of the cpu_baseline sample (the full batch, repeated)")
     a = ap.parse_args()
@@ -1109,7 +1110,8 @@ def main():
     call_ms = float(np.mean([ev[k].elapsed_ms(ev[k + 1]) for k in range(nlat)]))
 
     # HIP events around the dominant kernel on a spread sample of the timed steps (every M-th):
-    # each pair of records adds ~25 us to the cipher stream's step
+    # (AES suites: the events of the cipher kernel's own dispatch; event records of their own around
+    # a call cost ~25 us of the stream each pair)
     ev_steps = event_steps(args.steps, args.kernel_events_every)
     kev = {k: (Event(), Event()) for k in ev_steps}
     # RC4 / 3DES-only batches (cfg5) have no phases to overlap: their per-variant seal
@@ -1313,7 +1315,8 @@ def main():
                                            "span": ("the first variant's whole tlsgpu_seal_dev call on its stream "
                                                     "(prefix, MAC and cipher kernels: conservative for the "
                                                     "cipher kernel alone)") if conc else
-                                                   "the cipher kernel alone (tlsgpu_pipeline_seal's cipher events)"},
+                                                   "the cipher kernel alone (tlsgpu_pipeline_seal's cipher events: "
+                                                   "the kernel dispatch's own start / end, hipExtLaunchKernelGGL)"},
                          "kernel_ms_steps": {"first": round(per_launch[0], 4),
                                              "median": round(float(np.median(per_launch)), 4),
                                              "last": round(per_launch[-1], 4),

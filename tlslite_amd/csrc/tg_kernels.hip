@@ -23,6 +23,7 @@
 #include "tg_frame.h"
 #include "tg_derive.h"
 #include "tg_launch.h"
+#include <hip/hip_ext.h>
 #include <string>
 
 namespace tg {
@@ -466,10 +467,26 @@ static hipError_t launch_mac_phase(const tlsgpu_chain* chains, uint32_t nchains,
 }
 
 // phase 2 (stream s2, after phase 1): CBC over [explicit IV | P blocks | tail]
+// A cipher-phase kernel launch; with both events given, the events are those of the kernel's own
+// dispatch (hipExtLaunchKernelGGL: start and end of the kernel itself, no event packets of their
+// own on the stream between kernels -- the bench's sampled kernel times)
+template <typename K, typename... A>
+static void launch_timed(K kern, dim3 grid, dim3 block, uint32_t shm, hipStream_t s, hipEvent_t t0, hipEvent_t t1,
+                         A... args) {
+    if (t0 && t1) {
+        hipExtLaunchKernelGGL(kern, grid, block, shm, s, t0, t1, 0, args...);
+        return;
+    }
+    if (t0) (void)hipEventRecord(t0, s);  // one event alone: a record of its own on the stream
+    hipLaunchKernelGGL(kern, grid, block, shm, s, args...);
+    if (t1) (void)hipEventRecord(t1, s);
+}
+
 template <int NR>
 static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains, const tlsgpu_record* recs,
                                    uint32_t nrecords, const uint8_t* pt, uint8_t* wire, ConnState* states,
-                                   uint8_t* ws, uint32_t epoch, hipStream_t s, uint32_t nstates) {
+                                   uint8_t* ws, uint32_t epoch, hipStream_t s, uint32_t nstates,
+                                   hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr) {
     const uint32_t ncu = cu_count(s);
     RecMeta* meta = reinterpret_cast<RecMeta*>(ws);
     uint8_t* tails = ws + (size_t)nrecords * sizeof(RecMeta);
@@ -478,8 +495,8 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         pw = pw < 1 ? 1 : (pw > (uint32_t)D4_CHAINS ? (uint32_t)D4_CHAINS : pw);
         hipError_t e = set_lds(tdes4_kernel, D4_LDS_BYTES, s);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(tdes4_kernel, dim3((nchains + pw - 1) / pw), dim3(D4_THREADS), D4_LDS_BYTES, s, chains,
-                           nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch, nstates);
+        launch_timed(tdes4_kernel, dim3((nchains + pw - 1) / pw), dim3(D4_THREADS), D4_LDS_BYTES, s, t0, t1, chains,
+                     nchains, recs, nrecords, pt, wire, states, meta, tails, pw, epoch, nstates);
         return hipGetLastError();
     } else {
         const bool many = many_chains(nchains, s);
@@ -495,8 +512,8 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
             if (e != hipSuccess) return e;
             uint32_t grid = (nchains + cpw - 1) / cpw;
             grid = grid > ncu ? ncu : grid;
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), AES_LDS_BYTES, s, chains, nchains, recs,
-                               nrecords, pt, wire, states, meta, tails, cpw, epoch, nstates);
+            launch_timed(kern, dim3(grid), dim3(64 * waves), AES_LDS_BYTES, s, t0, t1, chains, nchains, recs,
+                         nrecords, pt, wire, states, meta, tails, cpw, epoch, nstates);
             return hipGetLastError();
         }
         // fewer chains than the pair regime's (so at most one generation of C3_CHAINS per CU)
@@ -509,8 +526,8 @@ static hipError_t launch_cbc_phase(const tlsgpu_chain* chains, uint32_t nchains,
         // persistent: at most one workgroup per CU, quads loop over chain generations
         uint32_t grid = (nchains + cpw - 1) / cpw;
         grid = grid > ncu ? ncu : grid;
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(C3_THREADS), AES_LDS_BYTES, s, chains,
-                           nchains, recs, nrecords, pt, wire, states, meta, tails, cpw, epoch, nstates);
+        launch_timed(kern, dim3(grid), dim3(C3_THREADS), AES_LDS_BYTES, s, t0, t1, chains,
+                     nchains, recs, nrecords, pt, wire, states, meta, tails, cpw, epoch, nstates);
         return hipGetLastError();
     }
 }
@@ -564,10 +581,8 @@ hipError_t launch_seal_phases(uint32_t variant, const tlsgpu_chain* chains, uint
             if ((e = hipEventRecord(mac_done, s1)) != hipSuccess) return e;                                      \
             if ((e = hipStreamWaitEvent(s2, mac_done, 0)) != hipSuccess) return e;                               \
         }                                                                                                        \
-        if (cbc_start && (e = hipEventRecord(cbc_start, s2)) != hipSuccess) return e;                           \
-        e = launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s2, sb.nstates);  \
-        if (e == hipSuccess && cbc_stop) e = hipEventRecord(cbc_stop, s2);                                       \
-        return e;                                                                                                \
+        return launch_cbc_phase<NR>(chains, nchains, recs, nrecords, pt, wire, states, ws, epoch, s2, sb.nstates, \
+                                    cbc_start, cbc_stop);                                                        \
     }
     TG_SPLIT_VARIANTS(TG_PH)
 #undef TG_PH
